@@ -1,0 +1,97 @@
+"""Golden-fixture case table (shared by tools/make_goldens.py and the tests).
+
+Every case is a seeded synthetic input (``tomatis_audio_processor_amd.synth``)
+plus reference parameters.  ``bypass`` marks configurations outside the
+reference's 48 kHz-stereo guard, run through the guard bypass.
+Lengths are chosen so that standard-mode cases cover every tail residue class
+that matters (N - n_fft mod hop = 0, 9, 259, 777) and at least one case spans
+several 240000-sample limiter chunks.
+"""
+import numpy as np
+
+S48, S44, S96 = 48000, 44100, 96000
+
+CASES = [
+    # --- standard (src/process_tomatis.py) ---------------------------------
+    dict(name="std_c1_mono44k_2048_512", mode="standard", sr=S44, ch=1, N=441000,
+         seed=1, bypass=True, params=dict(gate_ui=50, n_fft=2048, hop=512)),
+    dict(name="std_48k_st_2048_512_tail259", mode="standard", sr=S48, ch=2,
+         N=288000 + 2048 + 259, seed=2, params=dict(gate_ui=50, n_fft=2048, hop=512)),
+    dict(name="std_48k_st_4096_2048_linear_gain", mode="standard", sr=S48, ch=2,
+         N=144000 + 4096 + 777, seed=3,
+         params=dict(gate_ui=50, gate_mode="linear", gate_offset=-90,
+                     output_gain_db=3.0)),
+    dict(name="std_44k_st_4096_1024_d0", mode="standard", sr=S44, ch=2,
+         N=176400 + 4096 + 9, seed=4, bypass=True,
+         params=dict(gate_ui=50, n_fft=4096, hop=1024, up_delay_ms=0.0,
+                     hysteresis_db=2.0)),
+    dict(name="std_96k_st_4096_1024_tail0", mode="standard", sr=S96, ch=2,
+         N=4096 + 1024 * 230, seed=5, bypass=True,
+         params=dict(gate_ui=50, n_fft=4096, hop=1024)),
+    dict(name="std_48k_st_nolimit", mode="standard", sr=S48, ch=2, N=150000,
+         seed=6, params=dict(gate_ui=30, n_fft=2048, hop=512, output_gain_db=-12.0)),
+    dict(name="std_48k_st_hop300", mode="standard", sr=S48, ch=2, N=96000,
+         seed=7, params=dict(gate_ui=50, n_fft=2048, hop=300)),
+    dict(name="std_48k_st_short", mode="standard", sr=S48, ch=2, N=3000,
+         seed=8, params=dict(gate_ui=0, n_fft=2048, hop=512)),
+    # --- xfade (src/process_tomatis_xfade.py) ------------------------------
+    dict(name="xfade_48k_st_2048_512_500ms", mode="xfade", sr=S48, ch=2,
+         N=288000 + 5000, seed=11,
+         params=dict(gate_ui=50, gate_offset=-90, n_fft=2048, hop=512,
+                     xfade_ms=500.0)),
+    dict(name="xfade_96k_st_4096_1024_500ms", mode="xfade", sr=S96, ch=2,
+         N=96000 * 3 + 333, seed=12, bypass=True,
+         params=dict(gate_ui=50, gate_offset=-90, n_fft=4096, hop=1024,
+                     xfade_ms=500.0)),
+    dict(name="xfade_48k_st_0ms", mode="xfade", sr=S48, ch=2, N=120000, seed=13,
+         params=dict(gate_ui=50, gate_offset=-90, n_fft=2048, hop=512,
+                     xfade_ms=0.0)),
+    # --- adaptive (src/process_tomatis_adaptive.py) ------------------------
+    dict(name="adapt_44k_st_2048_512", mode="adaptive", sr=S44, ch=2, N=44100 * 8,
+         seed=21, params=dict(n_fft=2048, hop=512)),
+    dict(name="adapt_44k_st_quiet_f64", mode="adaptive", sr=S44, ch=2,
+         N=44100 * 6 + 123, seed=22, in_scale=0.01, params=dict(n_fft=2048, hop=512)),
+    dict(name="adapt_48k_mono_4096_2048", mode="adaptive", sr=S48, ch=1,
+         N=48000 * 7, seed=23, params=dict()),
+    # --- layer 2 (src/layer2_apply_eq.py) -----------------------------------
+    dict(name="l2_48k_st_pad_gp", mode="layer2", sr=S48, ch=2, N=150000 + 17,
+         seed=31, params=dict(n_fft=2048, hop=512)),
+    dict(name="l2_48k_st_nopad_gain", mode="layer2", sr=S48, ch=2, N=100000,
+         seed=32, params=dict(pad=False, global_gain_db=-6.0,
+                              auto_gain_protect=False)),
+    # --- layer 2b (src/layer2b_apply_residual_eq*.py) -----------------------
+    dict(name="l2b_96k_st_4096_1024", mode="layer2b", sr=S96, ch=2,
+         N=96000 * 2 + 1500, seed=41, params=dict(n_fft=4096, hop=1024)),
+    dict(name="l2b_safe_48k_st", mode="layer2b_safe", sr=S48, ch=2, N=120000,
+         seed=42, params=dict(n_fft=2048, hop=512)),
+]
+
+BY_NAME = {c["name"]: c for c in CASES}
+
+
+def eq_curve(n=48):
+    """Synthetic layer-2 EQ curve (freq_hz, delta_db), float-exact formula."""
+    f = np.geomspace(20.0, 20000.0, n)
+    d = 4.0 * np.sin(np.linspace(0.0, 3.0 * np.pi, n)) - 1.5
+    return f, d
+
+
+def eq_csv_rows(case=None):
+    f, d = eq_curve()
+    lines = ["freq_hz,delta_db"] + [f"{float(a)!r},{float(b)!r}" for a, b in zip(f, d)]
+    return "\n".join(lines) + "\n"
+
+
+def diff_curve(sr=48000, n_fft=4096):
+    """Synthetic ``diff_spectrum.csv`` in compare_audio.py's layout."""
+    freqs = np.fft.rfftfreq(n_fft, 1 / sr)
+    lf = np.log10(np.maximum(freqs, 1.0))
+    d = 5.0 * np.sin(2.1 * lf) + 1.5 * np.cos(37.0 * lf) - 0.5
+    return freqs, d
+
+
+def diff_csv_rows(case=None):
+    f, d = diff_curve()
+    lines = ["freq_hz,delta_db_base_minus_cand"]
+    lines += ["%.18e,%.18e" % (a, b) for a, b in zip(f, d)]
+    return "\n".join(lines) + "\n"
