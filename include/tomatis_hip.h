@@ -1,0 +1,176 @@
+/*
+ * tomatis_hip.h — C ABI of the MI355X (gfx950) STFT-gate-OLA engine.
+ *
+ * Drop-in boundary for the per-frame loop of the reference
+ * (xyjk0511/tomatis-audio-processor).  The reference has no FFI: its
+ * "operator API" is the set of Python functions below, each of which the
+ * Python host layer (tomatis_audio_processor_amd/) re-exposes under the same
+ * name and semantics and implements with these entry points:
+ *
+ *   reference                                   replaced by
+ *   ------------------------------------------- -------------------------------
+ *   src/process_tomatis.py:359-371 (frame loop:  tomatis_levels
+ *       power-mono RMS per frame, rms_dbfs
+ *       src/process_tomatis.py:43-52)
+ *   src/process_tomatis_adaptive.py:57-84        tomatis_levels
+ *       (compute_frame_levels)
+ *   src/process_tomatis.py:373-385 (gate)        tomatis_gate_std
+ *   src/process_tomatis_xfade.py:237-274         tomatis_gate_std (+alpha rows)
+ *   src/process_tomatis_adaptive.py:87-154       tomatis_minhold_bisect
+ *       (simulate_gate, find_optimal_threshold)
+ *   src/process_tomatis_adaptive.py:253-265      tomatis_minhold_bisect (alpha)
+ *   src/process_tomatis.py:394-406,419-426,451   tomatis_stft_ola
+ *       (rfft*gain, irfft*win, OLA, normalise)
+ *   src/process_tomatis_xfade.py:277-290         tomatis_stft_ola
+ *   src/process_tomatis_adaptive.py:298-338      tomatis_stft_ola
+ *   src/layer2_apply_eq.py:143-214               tomatis_stft_ola
+ *   src/layer2b_apply_residual_eq.py:120-160     tomatis_stft_ola
+ *   src/process_tomatis.py:331-357 (limiter),    tomatis_apply_limiter
+ *   src/process_tomatis_adaptive.py:340-345
+ *   np.max(np.abs(x)) (adaptive :201,          tomatis_absmax
+ *       layer2 gain protect :178,213)
+ *
+ * Conventions: every call is asynchronous on the given hipStream_t and returns
+ * an int status (0 = ok, <0 = error, see TOMATIS_E_*); no exceptions cross the
+ * ABI.  The caller owns every data buffer (device pointers, e.g. torch tensors'
+ * data_ptr()).  The library owns only the plan (host tables + small device
+ * workspace).  One plan per host thread / stream.  Layouts are documented in
+ * DESIGN.md ("Data layout in HBM").
+ */
+#ifndef TOMATIS_HIP_H
+#define TOMATIS_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TOMATIS_ABI_VERSION 1
+
+#define TOMATIS_OK 0
+#define TOMATIS_E_ARG (-1)        /* bad argument */
+#define TOMATIS_E_UNSUPPORTED (-2)/* shape/config not built for gfx950 here */
+#define TOMATIS_E_HIP (-3)        /* a HIP runtime call failed */
+#define TOMATIS_E_NOMEM (-4)
+
+/* OLA normalisation rule */
+#define TOMATIS_NORM_EPS 0        /* y = ola / (wsum + 1e-12f)   (standard, xfade, layer2, layer2b) */
+#define TOMATIS_NORM_MAX 1        /* y = ola / max(wsum, 1e-8f)  (adaptive) */
+
+/* Per-frame level precision (reference dtype) */
+#define TOMATIS_F32 0
+#define TOMATIS_F64 1
+
+/* Per-stream geometry + gate parameters.  All positions are in samples of the
+ * stream's own time axis, where samples [0, n) are the input and everything
+ * outside is zero (the reference's padding).  Frame k covers
+ * [first_start + k*hop, first_start + k*hop + n_fft). */
+typedef struct TomatisStream {
+    int64_t in_off;       /* float index of sample 0 / channel 0 in x          */
+    int64_t out_off;      /* float index of output sample 0 / channel 0 in y   */
+    int64_t n;            /* input samples per channel                          */
+    int64_t first_start;  /* position of frame 0                                */
+    int64_t n_frames;     /* frames of this stream                              */
+    int64_t out_begin;    /* position of output sample 0                        */
+    int64_t out_len;      /* output samples per channel                         */
+    int64_t chunk_first;  /* position where limiter chunk 1 starts              */
+    int64_t chunk_len;    /* length of chunks 1..n_chunks-2 (last runs to end)  */
+    int32_t n_chunks;     /* limiter chunks (>=1)                               */
+    float in_scale;       /* x is multiplied by this (f32) before framing       */
+    float out_scale;      /* y is multiplied by this (f32) before the peak      */
+    /* standard gate on float32 r bit patterns:
+     *   on  = (bits >= on_bits)  XOR (bits in on_exc[0..n_on_exc))
+     *   off = (bits <= off_bits) XOR (bits in off_exc[0..n_off_exc))
+     * NaN r -> both false. */
+    uint32_t on_bits, off_bits;
+    uint32_t on_exc[4], off_exc[4];
+    int32_t n_on_exc, n_off_exc;
+    /* f64 thresholds (min-hold gate on f64 levels) */
+    double t_on, t_off;
+    /* filled by tomatis_plan_create: */
+    int64_t frame_base;   /* index of frame 0 in per-frame arrays               */
+    int32_t chunk_base;   /* index of chunk 0 in per-chunk arrays               */
+    int32_t _pad;
+} TomatisStream;
+
+typedef struct TomatisPlanDesc {
+    int32_t n_fft;        /* 2048 or 4096 on the fast path                      */
+    int32_t hop;          /* any 1..n_fft; fast OLA when hop % (n_fft/32) == 0  */
+    int32_t ch;           /* 1 or 2                                             */
+    int32_t norm_mode;    /* TOMATIS_NORM_*                                     */
+    int32_t up_delay_frames; /* ceil(up_delay_samples/hop), >=0 (standard gate) */
+    int32_t min_hold_frames; /* adaptive min-hold                               */
+    int32_t xfade_frames;    /* xfade / adaptive alpha step = 1/xfade_frames    */
+    int32_t alpha_mode;      /* 0 none, 1 xfade (python-float start), 2 adaptive */
+} TomatisPlanDesc;
+
+typedef struct tomatis_plan_s* tomatis_plan_t;
+
+/* Library / device info */
+int tomatis_abi_version(void);
+const char* tomatis_status_string(int status);
+
+/* Plan: copies the stream table (host array) to the device, assigns
+ * frame_base / chunk_base, builds window / twiddle / pairwise-sum tables and
+ * the work decompositions.  Returns TOMATIS_E_UNSUPPORTED for shapes the
+ * gfx950 kernels are not built for. */
+int tomatis_plan_create(tomatis_plan_t* plan, const TomatisPlanDesc* desc,
+                        const float* window /* host, n_fft floats: np.hanning(n_fft) as f32 */,
+                        TomatisStream* streams /* in/out, host */, int32_t n_streams);
+int tomatis_plan_destroy(tomatis_plan_t plan);
+int64_t tomatis_plan_total_frames(tomatis_plan_t plan);
+int32_t tomatis_plan_total_chunks(tomatis_plan_t plan);
+/* Re-upload per-stream gate / scale fields after the host changed them
+ * (adaptive thresholds, attenuation).  Geometry must be unchanged. */
+int tomatis_plan_update_streams(tomatis_plan_t plan, const TomatisStream* streams,
+                                void* hip_stream);
+
+/* Per-frame RMS r (reference rms_dbfs before the log10): float32 (prec=F32)
+ * or float64 (prec=F64) per frame, frame-major over all streams. */
+int tomatis_levels(tomatis_plan_t plan, const float* x, void* r_out, int32_t prec,
+                   void* hip_stream);
+
+/* Standard / xfade gate: states (1=C1, 2=C2) per frame and the gain-row index
+ * per frame for tomatis_stft_ola.  Rows: 0 = g1, 1 = g2, 2+m = mixed gain at
+ * alpha = m/xfade_frames (alpha_mode 1).  alpha_out (optional, f64 per frame). */
+int tomatis_gate_std(tomatis_plan_t plan, const float* r, uint8_t* states,
+                     uint16_t* rows, double* alpha_out, void* hip_stream);
+
+/* Adaptive: bisection for the min-hold threshold per stream
+ * (find_optimal_threshold), final states, alpha and gain rows (2+m).
+ * levels: f64 per frame; t_lo_hi_med: 3 doubles per stream (p5, p95, median of
+ * valid levels; n_valid==0 streams pass NaN and get t = median(levels) in
+ * t_lo_hi_med[2]); target_c2, hyst_db as in the reference. */
+int tomatis_minhold_bisect(tomatis_plan_t plan, const double* levels,
+                           const double* t_lo_hi_med, double target_c2, double hyst_db,
+                           double* t_out, uint8_t* states, uint16_t* rows,
+                           double* alpha_out, void* hip_stream);
+
+/* Fused framing -> window -> FFT -> gain row -> IFFT -> window -> OLA ->
+ * normalise -> out_scale, plus per-chunk |y| maxima as float bits
+ * (chunk_peak_bits must be zeroed by the caller; uint32 per chunk). */
+int tomatis_stft_ola(tomatis_plan_t plan, const float* x, const float* gain_rows,
+                     int32_t n_rows, const uint16_t* rows, float* y,
+                     uint32_t* chunk_peak_bits, void* hip_stream);
+
+/* Limiter fix-up: chunk j of every stream is multiplied by limit/peak_j
+ * (float32 division, as the reference) when peak_j > limit. */
+int tomatis_apply_limiter(tomatis_plan_t plan, float* y, const uint32_t* chunk_peak_bits,
+                          float limit, void* hip_stream);
+
+/* max |x| over n floats as float bits (out zeroed by caller). */
+int tomatis_absmax(const float* x, int64_t n, uint32_t* out_bits, void* hip_stream);
+
+/* y[i] = x[i] * scale (float32), n floats (layer-2 gain-protect copy). */
+int tomatis_scale_copy(const float* x, float* y, int64_t n, float scale, void* hip_stream);
+
+/* Deterministic synthetic PCM (twin of tomatis_audio_processor_amd/synth.py):
+ * samples [start, start+n) of stream `seed`, ch channels, interleaved. */
+int tomatis_synth_fill(float* x, int64_t n, int32_t ch, int32_t sr, uint32_t seed,
+                       int64_t start, void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TOMATIS_HIP_H */

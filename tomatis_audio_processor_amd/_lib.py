@@ -1,0 +1,126 @@
+"""ctypes binding of the gfx950 C-ABI library ``libtomatis_hip.so``.
+
+The library is the product: there is no CPU fallback.  ``lib()`` raises
+``TomatisLibraryError`` when the shared object is missing or fails to load, and
+every entry point's int status is turned into an exception by ``check``.
+
+``torch`` is imported (when available) *before* the library is loaded so that
+the process holds a single HIP runtime: torch's bundled ``libamdhip64.so`` has
+the same SONAME (``libamdhip64.so.7``) as the one the library links against.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+LIB_NAME = "libtomatis_hip.so"
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+F32, F64 = 0, 1
+NORM_EPS, NORM_MAX = 0, 1
+
+
+class TomatisLibraryError(RuntimeError):
+    pass
+
+
+class TomatisStream(C.Structure):
+    """Mirror of ``TomatisStream`` in include/tomatis_hip.h."""
+    _fields_ = [
+        ("in_off", C.c_int64), ("out_off", C.c_int64), ("n", C.c_int64),
+        ("first_start", C.c_int64), ("n_frames", C.c_int64),
+        ("out_begin", C.c_int64), ("out_len", C.c_int64),
+        ("chunk_first", C.c_int64), ("chunk_len", C.c_int64),
+        ("n_chunks", C.c_int32), ("in_scale", C.c_float), ("out_scale", C.c_float),
+        ("on_bits", C.c_uint32), ("off_bits", C.c_uint32),
+        ("on_exc", C.c_uint32 * 4), ("off_exc", C.c_uint32 * 4),
+        ("n_on_exc", C.c_int32), ("n_off_exc", C.c_int32),
+        ("t_on", C.c_double), ("t_off", C.c_double),
+        ("frame_base", C.c_int64), ("chunk_base", C.c_int32), ("_pad", C.c_int32),
+    ]
+
+
+class TomatisPlanDesc(C.Structure):
+    _fields_ = [
+        ("n_fft", C.c_int32), ("hop", C.c_int32), ("ch", C.c_int32),
+        ("norm_mode", C.c_int32), ("up_delay_frames", C.c_int32),
+        ("min_hold_frames", C.c_int32), ("xfade_frames", C.c_int32),
+        ("alpha_mode", C.c_int32),
+    ]
+
+
+_P = C.c_void_p
+_SIGS = {
+    "tomatis_abi_version": (C.c_int, []),
+    "tomatis_status_string": (C.c_char_p, [C.c_int]),
+    "tomatis_plan_create": (C.c_int, [C.POINTER(_P), C.POINTER(TomatisPlanDesc),
+                                      C.POINTER(C.c_float), C.POINTER(TomatisStream),
+                                      C.c_int32]),
+    "tomatis_plan_destroy": (C.c_int, [_P]),
+    "tomatis_plan_total_frames": (C.c_int64, [_P]),
+    "tomatis_plan_total_chunks": (C.c_int32, [_P]),
+    "tomatis_plan_update_streams": (C.c_int, [_P, C.POINTER(TomatisStream), _P]),
+    "tomatis_levels": (C.c_int, [_P, _P, _P, C.c_int32, _P]),
+    "tomatis_gate_std": (C.c_int, [_P, _P, _P, _P, _P, _P]),
+    "tomatis_minhold_bisect": (C.c_int, [_P, _P, _P, C.c_double, C.c_double, _P, _P, _P,
+                                         _P, _P]),
+    "tomatis_stft_ola": (C.c_int, [_P, _P, _P, C.c_int32, _P, _P, _P, _P]),
+    "tomatis_apply_limiter": (C.c_int, [_P, _P, _P, C.c_float, _P]),
+    "tomatis_absmax": (C.c_int, [_P, C.c_int64, _P, _P]),
+    "tomatis_scale_copy": (C.c_int, [_P, _P, C.c_int64, C.c_float, _P]),
+    "tomatis_synth_fill": (C.c_int, [_P, C.c_int64, C.c_int32, C.c_int32, C.c_uint32,
+                                     C.c_int64, _P]),
+}
+EXPORTS = tuple(_SIGS)
+
+_LIB = None
+
+
+def lib_path() -> str:
+    return os.environ.get("TOMATIS_HIP_LIB", os.path.join(HERE, LIB_NAME))
+
+
+def lib():
+    """Load (once) and return the ctypes handle; raise if it cannot be loaded."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    path = lib_path()
+    if not os.path.exists(path):
+        raise TomatisLibraryError(
+            f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            " (hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    try:
+        import torch  # noqa: F401  (single HIP runtime, see module docstring)
+    except Exception:  # pragma: no cover - torch is part of the image
+        pass
+    try:
+        h = C.CDLL(path, mode=C.RTLD_GLOBAL)
+    except OSError as e:
+        raise TomatisLibraryError(f"cannot load {path}: {e}") from e
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(h, name)
+        fn.restype = res
+        fn.argtypes = args
+    if h.tomatis_abi_version() != 1:
+        raise TomatisLibraryError("ABI version mismatch")
+    _LIB = h
+    return h
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().tomatis_status_string(rc).decode()
+        raise RuntimeError(f"{what or 'tomatis'} failed: {msg} (status {rc})")
+
+
+def ptr(t) -> C.c_void_p:
+    """Device pointer of a torch tensor (or None -> NULL)."""
+    if t is None:
+        return C.c_void_p(0)
+    return C.c_void_p(t.data_ptr())
+
+
+def stream_handle(device=None) -> C.c_void_p:
+    import torch
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)

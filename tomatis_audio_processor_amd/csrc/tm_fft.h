@@ -1,0 +1,196 @@
+// tm_fft.h — N = 32*P point complex FFT held in registers of P lanes
+// (32 complex values per lane), exchanged through LDS, for gfx950 wave64.
+//
+// Decomposition (four-step, then the P-point step split 8 x PB):
+//   n = n1 + P*n2            (n1 = lane, n2 = register)         step 1: DFT_32 over n2
+//   twiddle W_N^{n1*k2}                                          step 2
+//   n1 = a + 8*b, k1 = c + PB*d, k = k2 + 32*k1
+//   step 3a: DFT_PB over b   lanes (a = L%8, q = L/8), regs (j, b), k2 = q + PB*j
+//   step 3b: twiddle W_P^{a*c}
+//   step 3c: DFT_8 over a    lanes (c = L%PB, q' = L/PB), regs (j', d), k2 = q' + 8*j'
+// After the forward transform lane (c, q') register j'*8+d holds bin
+//   k = (q' + 8 j') + 32 (c + PB d).
+// The inverse walks the same steps backwards with conjugate twiddles and ends
+// with lane L register n2 holding sample L + P*n2 (the OLA-friendly layout).
+// Exchanges go through an LDS round buffer of PB rows x (P+8) complex; rounds
+// cover k2 blocks of PB so a round reads back exactly the registers it wrote.
+#pragma once
+#include "tm_common.h"
+
+namespace tdsp {
+
+template <int P_>
+struct FftGeo {
+  static constexpr int P = P_;
+  static constexpr int NR = 32;             // complex registers per lane
+  static constexpr int N = NR * P;          // transform size
+  static constexpr int PB = P / 8;          // step-3a size
+  static constexpr int NJ = NR / PB;        // step-3a transforms per lane
+  static constexpr int RW = P + 8;          // LDS row stride (complex)
+  static constexpr int ROUNDS = NR / PB;    // exchange rounds
+  static constexpr int BUF = PB * RW;       // complex per round buffer
+  static_assert(PB >= 4 && PB <= 32, "P in [32, 256]");
+};
+
+// LDS synchronisation for an exchange: wave-local when P == 64.
+template <int P>
+__device__ __forceinline__ void xsync() {
+  if constexpr (P <= 64) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  } else {
+    __syncthreads();
+  }
+}
+
+// exchange-2 column of element (a, c) in a row
+__device__ __forceinline__ int x2col(int a, int c) { return 8 * c + (a ^ (c & 7)); }
+
+// forward FFT.  v: 32 registers (input x[L + P*n2]); out: bin layout above.
+// twN: LDS [32][P] with W_N^{n1*k2}; twP: LDS [P] with W_P^m; buf: round buffer.
+template <int P>
+__device__ __forceinline__ void fft_fwd(cf (&v)[32], int L, const cf* twN, const cf* twP,
+                                        cf* buf) {
+  using G = FftGeo<P>;
+  constexpr int PB = G::PB, RW = G::RW;
+  const int a1 = L & 7, q1 = L >> 3;
+  const int c3 = L % PB, q3 = L / PB;
+  // step 1
+  dft<32, false, 0, 1, 32>(v);
+  // step 2
+  sfor<1, 32>([&](auto kk) {
+    constexpr int K = decltype(kk)::value;
+    v[K] = cmul(v[K], twN[K * P + L]);
+  });
+  // exchange 1 : (lane n1, reg k2) -> (lane (a,q), reg (j,b))
+  sfor<0, G::ROUNDS>([&](auto rr) {
+    constexpr int R = decltype(rr)::value;
+    sfor<0, PB>([&](auto kk) {
+      constexpr int K = decltype(kk)::value;
+      buf[K * RW + L] = v[R * PB + K];
+    });
+    xsync<P>();
+    sfor<0, PB>([&](auto bb) {
+      constexpr int B = decltype(bb)::value;
+      v[R * PB + B] = buf[q1 * RW + a1 + 8 * B];
+    });
+    xsync<P>();
+  });
+  // step 3a: DFT_PB over b for each j
+  sfor<0, G::NJ>([&](auto jj) {
+    constexpr int J = decltype(jj)::value;
+    dft<PB, false, J * PB, 1, 32>(v);
+  });
+  // step 3b: W_P^{a c}
+  sfor<1, PB>([&](auto cc) {
+    constexpr int C = decltype(cc)::value;
+    const cf w = twP[(a1 * C) & (P - 1)];
+    sfor<0, G::NJ>([&](auto jj) {
+      constexpr int J = decltype(jj)::value;
+      v[J * PB + C] = cmul(v[J * PB + C], w);
+    });
+  });
+  // exchange 2 : (lane (a,q), reg (j,c)) -> (lane (c,q'), reg (j',a))
+  sfor<0, G::ROUNDS>([&](auto rr) {
+    constexpr int R = decltype(rr)::value;
+    sfor<0, PB>([&](auto cc) {
+      constexpr int C = decltype(cc)::value;
+      buf[q1 * RW + x2col(a1, C)] = v[R * PB + C];
+    });
+    xsync<P>();
+    sfor<0, PB / 8>([&](auto jj) {
+      constexpr int JJ = decltype(jj)::value;
+      const int row = q3 + 8 * JJ;
+      sfor<0, 8>([&](auto aa) {
+        constexpr int A = decltype(aa)::value;
+        v[R * PB + JJ * 8 + A] = buf[row * RW + x2col(A, c3)];
+      });
+    });
+    xsync<P>();
+  });
+  // step 3c: DFT_8 over a
+  sfor<0, 4>([&](auto jj) {
+    constexpr int J = decltype(jj)::value;
+    dft<8, false, J * 8, 1, 32>(v);
+  });
+}
+
+// inverse (unnormalised) FFT: bin layout -> v[n2] = x[L + P*n2] * N
+template <int P>
+__device__ __forceinline__ void fft_inv(cf (&v)[32], int L, const cf* twN, const cf* twP,
+                                        cf* buf) {
+  using G = FftGeo<P>;
+  constexpr int PB = G::PB, RW = G::RW;
+  const int a1 = L & 7, q1 = L >> 3;
+  const int c3 = L % PB, q3 = L / PB;
+  // step 3c': IDFT_8 over d -> a
+  sfor<0, 4>([&](auto jj) {
+    constexpr int J = decltype(jj)::value;
+    dft<8, true, J * 8, 1, 32>(v);
+  });
+  // step 3b': conj W_P^{a c3}
+  sfor<1, 8>([&](auto aa) {
+    constexpr int A = decltype(aa)::value;
+    const cf w = twP[(A * c3) & (P - 1)];
+    sfor<0, 4>([&](auto jj) {
+      constexpr int J = decltype(jj)::value;
+      v[J * 8 + A] = cmulc(v[J * 8 + A], w);
+    });
+  });
+  // exchange 3 : (lane (c,q'), reg (j',a)) -> (lane (a,q), reg (j,c))
+  sfor<0, G::ROUNDS>([&](auto rr) {
+    constexpr int R = decltype(rr)::value;
+    sfor<0, PB / 8>([&](auto jj) {
+      constexpr int JJ = decltype(jj)::value;
+      const int row = q3 + 8 * JJ;
+      sfor<0, 8>([&](auto aa) {
+        constexpr int A = decltype(aa)::value;
+        buf[row * RW + x2col(A, c3)] = v[R * PB + JJ * 8 + A];
+      });
+    });
+    xsync<P>();
+    sfor<0, PB>([&](auto cc) {
+      constexpr int C = decltype(cc)::value;
+      v[R * PB + C] = buf[q1 * RW + x2col(a1, C)];
+    });
+    xsync<P>();
+  });
+  // step 3a': IDFT_PB over c -> b
+  sfor<0, G::NJ>([&](auto jj) {
+    constexpr int J = decltype(jj)::value;
+    dft<PB, true, J * PB, 1, 32>(v);
+  });
+  // exchange 4 : (lane (a,q), reg (j,b)) -> (lane n1, reg k2)
+  sfor<0, G::ROUNDS>([&](auto rr) {
+    constexpr int R = decltype(rr)::value;
+    sfor<0, PB>([&](auto bb) {
+      constexpr int B = decltype(bb)::value;
+      buf[q1 * RW + a1 + 8 * B] = v[R * PB + B];
+    });
+    xsync<P>();
+    sfor<0, PB>([&](auto kk) {
+      constexpr int K = decltype(kk)::value;
+      v[R * PB + K] = buf[K * RW + L];
+    });
+    xsync<P>();
+  });
+  // step 2': conj W_N^{n1 k2}
+  sfor<1, 32>([&](auto kk) {
+    constexpr int K = decltype(kk)::value;
+    v[K] = cmulc(v[K], twN[K * P + L]);
+  });
+  // step 1': IDFT_32 over k2 -> n2
+  dft<32, true, 0, 1, 32>(v);
+}
+
+// bin index held by lane L, register index i (= j'*8 + d) after fft_fwd
+template <int P>
+__device__ __forceinline__ int fft_bin(int L, int i) {
+  constexpr int PB = P / 8;
+  const int c3 = L % PB, q3 = L / PB;
+  const int jp = i >> 3, d = i & 7;
+  return (q3 + 8 * jp) + 32 * (c3 + PB * d);
+}
+
+}  // namespace tdsp

@@ -1,0 +1,1245 @@
+// tm_kernels.hip — gfx950 kernels + C ABI of the STFT-gate-OLA engine.
+//
+// Reference semantics (xyjk0511/tomatis-audio-processor, file:line):
+//   levels        src/process_tomatis.py:43-52,369-371  (power-mono RMS, numpy pairwise mean)
+//   gate (std)    src/process_tomatis.py:373-385         (hysteresis + up-delay)
+//   alpha (xfade) src/process_tomatis_xfade.py:251-274
+//   gate (minhold) + bisection  src/process_tomatis_adaptive.py:87-154
+//   alpha (adaptive)            src/process_tomatis_adaptive.py:253-265
+//   STFT/OLA      src/process_tomatis.py:394-406 ; normalise :422,452 ; limiter :331-357
+//   adaptive OLA  src/process_tomatis_adaptive.py:298-345
+//   layer-2(b)    src/layer2_apply_eq.py:143-214 ; src/layer2b_apply_residual_eq.py:120-160
+// Design: DESIGN.md.  Compiled with -ffp-contract=off: every FMA below is explicit.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "tm_common.h"
+#include "tm_fft.h"
+#include "../../include/tomatis_hip.h"
+
+using namespace tdsp;
+
+namespace {
+
+constexpr float kEps32 = 1e-12f;     // EPS as the reference adds it to float32 arrays
+constexpr double kEps64 = 1e-12;
+constexpr int kSeg = 1024;           // gate segment length (frames)
+constexpr int kMhSeg = 256;          // min-hold segment length (frames)
+constexpr int kLevelLds = 12288;     // floats of LDS for the levels span
+constexpr int kMaxGateStates = 1024;
+
+struct Run {          // main-kernel work item: emit frames [ka, kb) of stream s
+  int32_t s;
+  int32_t last;       // 1 if kb is the stream's last frame + 1
+  int64_t ka, kb;
+};
+struct LvlBlock {     // levels work item
+  int32_t s;
+  int32_t nf;
+  int64_t k0;
+};
+struct GateSeg {      // gate segment
+  int32_t s;
+  int32_t nf;
+  int64_t k0;         // first frame (stream-local)
+};
+
+__device__ __forceinline__ int64_t floordiv(int64_t a, int64_t b) {
+  int64_t q = a / b;
+  return (q * b > a) ? q - 1 : q;
+}
+
+// ===========================================================================
+// Levels: r = sqrt(mean(m*m) + EPS), m = sqrt(mean_c(x_c^2)), numpy pairwise
+// ===========================================================================
+template <typename T>
+__device__ __forceinline__ T msq_of(const float* xs, int ch, T scale);
+
+template <>
+__device__ __forceinline__ float msq_of<float>(const float* xs, int ch, float scale) {
+  // frame**2 -> mean over channels (sequential from 0, n<8 pairwise branch) -> sqrt -> square
+  float acc = 0.f;
+  for (int c = 0; c < ch; ++c) {
+    const float v = xs[c] * scale;
+    acc = acc + v * v;
+  }
+  const float mean = (ch == 1) ? acc : ((ch == 2) ? acc * 0.5f : acc / (float)ch);
+  const float m = sqrtf(mean);
+  return m * m;
+}
+template <>
+__device__ __forceinline__ double msq_of<double>(const float* xs, int ch, double scale) {
+  double acc = 0.0;
+  for (int c = 0; c < ch; ++c) {
+    const double v = (double)xs[c] * scale;
+    acc = acc + v * v;
+  }
+  const double mean = (ch == 1) ? acc : ((ch == 2) ? acc * 0.5 : acc / (double)ch);
+  const double m = sqrt(mean);
+  return m * m;
+}
+
+// padded LDS index (one 4-element pad per 128 elements -> conflict-free b128 leaf reads)
+template <bool PAD>
+__device__ __forceinline__ int lidx(int i) {
+  if constexpr (PAD) return i + 4 * (i >> 7);
+  else return i;
+}
+
+// numpy pairwise block for n == 128 (8 accumulators, then a fixed tree)
+template <typename T, bool PAD>
+__device__ __forceinline__ T leaf128(const T* lds, int start) {
+  T r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = lds[lidx<PAD>(start + j)];
+#pragma unroll
+  for (int i = 8; i < 128; i += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = r[j] + lds[lidx<PAD>(start + i + j)];
+  }
+  return ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+}
+
+template <typename T, bool PAD>
+__global__ __launch_bounds__(256) void k_levels(const float* __restrict__ x,
+                                                const TomatisStream* __restrict__ st,
+                                                const LvlBlock* __restrict__ blocks, int n_fft,
+                                                int hop, int ch, T* __restrict__ r_out) {
+  __shared__ T lds[kLevelLds * sizeof(float) / sizeof(T) + 256];
+  __shared__ T leaves[1024];
+  const LvlBlock blk = blocks[blockIdx.x];
+  const TomatisStream S = st[blk.s];
+  const int64_t span0 = S.first_start + blk.k0 * hop;
+  const int span = (blk.nf - 1) * hop + n_fft;
+  const T scale = (T)S.in_scale;
+  const float* xs = x + S.in_off;
+  for (int i = threadIdx.x; i < span; i += blockDim.x) {
+    const int64_t p = span0 + i;
+    T v = (T)0;
+    if (p >= 0 && p < S.n) v = msq_of<T>(xs + p * ch, ch, scale);
+    lds[lidx<PAD>(i)] = v;
+  }
+  __syncthreads();
+  const int nleaf = n_fft >> 7;  // n_fft power of two >= 256
+  const int total = blk.nf * nleaf;
+  for (int t = threadIdx.x; t < total; t += blockDim.x) {
+    const int f = t / nleaf, l = t - f * nleaf;
+    leaves[t] = leaf128<T, PAD>(lds, f * hop + 128 * l);
+  }
+  __syncthreads();
+  if (threadIdx.x < blk.nf) {
+    T* lv = leaves + threadIdx.x * nleaf;
+    for (int w = nleaf; w > 1; w >>= 1)
+      for (int i = 0; i < w / 2; ++i) lv[i] = lv[2 * i] + lv[2 * i + 1];
+    const T sum = lv[0];
+    const T mean = sum / (T)n_fft;
+    const T r = sqrt(mean + (T)(sizeof(T) == 4 ? (double)kEps32 : kEps64));
+    r_out[S.frame_base + blk.k0 + threadIdx.x] = r;
+  }
+}
+
+// ===========================================================================
+// Standard gate (process_tomatis.py:373-385) as a transfer-function scan.
+// state id: 0 = C1 idle, 1..D = C1 pending for (id-1) frames, D+1 = C2.
+// ===========================================================================
+__device__ __forceinline__ bool in_exc(uint32_t b, const uint32_t* e, int n) {
+  bool hit = false;
+  for (int i = 0; i < n; ++i) hit |= (b == e[i]);
+  return hit;
+}
+__device__ __forceinline__ uint8_t gate_pred(float r, const TomatisStream& S) {
+  const uint32_t b = __float_as_uint(r);
+  if (r != r) return 0;
+  const bool on = (b >= S.on_bits) != in_exc(b, S.on_exc, S.n_on_exc);
+  const bool off = (b <= S.off_bits) != in_exc(b, S.off_exc, S.n_off_exc);
+  return (uint8_t)((on ? 1 : 0) | (off ? 2 : 0));
+}
+__device__ __forceinline__ int gate_step(int id, uint8_t pr, int D) {
+  if (id == D + 1) return (pr & 2) ? 0 : id;
+  if (pr & 1) {
+    const int age = (id == 0) ? 0 : id;  // frames since pending was set, after this frame
+    return (age >= D) ? D + 1 : age + 1;
+  }
+  return 0;
+}
+
+__global__ __launch_bounds__(256) void k_gate_tf(const float* __restrict__ r,
+                                                 const TomatisStream* __restrict__ st,
+                                                 const GateSeg* __restrict__ segs, int nseg,
+                                                 int D, uint16_t* __restrict__ tf) {
+  __shared__ uint8_t pr[4][kSeg];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int sg = blockIdx.x * 4 + wv;
+  if (sg >= nseg) return;
+  const GateSeg G = segs[sg];
+  const TomatisStream S = st[G.s];
+  for (int i = lane; i < G.nf; i += 64) pr[wv][i] = gate_pred(r[S.frame_base + G.k0 + i], S);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int ns = D + 2;
+  for (int s0 = 0; s0 < ns; s0 += 64) {
+    int id = s0 + lane;
+    if (id < ns) {
+      for (int i = 0; i < G.nf; ++i) id = gate_step(id, pr[wv][i], D);
+      tf[(int64_t)sg * ns + s0 + lane] = (uint16_t)id;
+    }
+  }
+}
+
+// sequential composition over a stream's segments (one thread per stream)
+__global__ void k_gate_chain(const TomatisStream* __restrict__ st, int n_streams,
+                             const int32_t* __restrict__ seg_first,
+                             const int32_t* __restrict__ seg_count, int ns,
+                             const uint16_t* __restrict__ tf, uint16_t* __restrict__ seg_start,
+                             int init_id) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_streams) return;
+  int id = init_id;
+  const int a = seg_first[s], n = seg_count[s];
+  for (int i = 0; i < n; ++i) {
+    seg_start[a + i] = (uint16_t)id;
+    id = tf[(int64_t)(a + i) * ns + id];
+  }
+}
+
+// one wave per segment: lanes evaluate 64 predicates at a time, the automaton
+// advances on the (wave-uniform) scalar path, lane i keeps the state of frame i
+__global__ __launch_bounds__(256) void k_gate_resolve(const float* __restrict__ r,
+                                                      const TomatisStream* __restrict__ st,
+                                                      const GateSeg* __restrict__ segs, int nseg,
+                                                      int D, const uint16_t* __restrict__ seg_start,
+                                                      uint8_t* __restrict__ states,
+                                                      uint16_t* __restrict__ rows) {
+  const int lane = threadIdx.x & 63;
+  const int sg = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (sg >= nseg) return;
+  const GateSeg G = segs[sg];
+  const TomatisStream S = st[G.s];
+  int id = seg_start[sg];
+  const int64_t f0 = S.frame_base + G.k0;
+  for (int base = 0; base < G.nf; base += 64) {
+    const int i = base + lane;
+    const int pr = (i < G.nf) ? (int)gate_pred(r[f0 + i], S) : 0;
+    const int cnt = min(64, G.nf - base);
+    int mine = 0;
+    for (int t = 0; t < cnt; ++t) {
+      const int pt = __builtin_amdgcn_readlane(pr, t);
+      id = gate_step(id, (uint8_t)pt, D);
+      mine = (lane == t) ? id : mine;
+    }
+    if (i < G.nf) {
+      const uint8_t stt = (mine == D + 1) ? 2 : 1;
+      states[f0 + i] = stt;
+      if (rows) rows[f0 + i] = (uint16_t)(stt - 1);
+    }
+  }
+}
+
+// ===========================================================================
+// alpha scans (sequential per stream; f64 exactly as the reference)
+// ===========================================================================
+__device__ __forceinline__ double alpha_step(double a, double tgt, double step) {
+  const double d = tgt - a;
+  if (fabs(d) <= step) return tgt;
+  return a + step * (d > 0 ? 1.0 : (d < 0 ? -1.0 : 0.0));
+}
+
+// xfade (process_tomatis_xfade.py:251-274): alpha starts at 0.0.
+__global__ void k_alpha_xfade(const TomatisStream* __restrict__ st, int n_streams,
+                              const uint8_t* __restrict__ states, int xf,
+                              uint16_t* __restrict__ rows, double* __restrict__ alpha) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_streams) return;
+  const TomatisStream S = st[s];
+  const double step = xf > 0 ? 1.0 / xf : 1.0;
+  double a = 0.0;
+  for (int64_t k = 0; k < S.n_frames; ++k) {
+    const int64_t f = S.frame_base + k;
+    const double tgt = states[f] == 1 ? 0.0 : 1.0;
+    a = (xf > 0) ? alpha_step(a, tgt, step) : tgt;
+    if (alpha) alpha[f] = a;
+    uint16_t row;
+    if (xf > 0 && a > 0.0 && a < 1.0) row = (uint16_t)(2 + (int)rint(a * xf));
+    else row = (a < 0.5) ? 0 : 1;
+    rows[f] = row;
+  }
+}
+
+// ===========================================================================
+// Adaptive: min-hold gate, bisection, final states, alpha (one block per stream)
+// state id = (C - 1) * (mh + 1) + min(since, mh)
+// ===========================================================================
+__device__ __forceinline__ int mh_step(int id, double lv, double ton, double toff, int mh) {
+  const int c2 = id / (mh + 1);
+  int since = id - c2 * (mh + 1);
+  since = min(since + 1, mh);
+  if (since >= mh) {
+    if (!c2) {
+      if (lv >= ton) return (mh + 1) * 1 + 0;
+    } else {
+      if (lv <= toff) return 0;
+    }
+  }
+  return c2 * (mh + 1) + since;
+}
+
+// workspace per stream: tf/cnt per (segment, state)
+__device__ void mh_simulate(const double* __restrict__ lv, int64_t F, double ton, double toff,
+                            int mh, uint16_t* __restrict__ tf, int32_t* __restrict__ cnt) {
+  const int ns = 2 * (mh + 1);
+  const int nseg = (int)((F + kMhSeg - 1) / kMhSeg);
+  const int nwork = nseg * ns;
+  for (int w = threadIdx.x; w < nwork; w += blockDim.x) {
+    const int sg = w / ns, s0 = w - sg * ns;
+    const int64_t k0 = (int64_t)sg * kMhSeg;
+    const int nf = (int)min<int64_t>(kMhSeg, F - k0);
+    int id = s0, c = 0;
+    for (int i = 0; i < nf; ++i) {
+      id = mh_step(id, lv[k0 + i], ton, toff, mh);
+      c += (id > mh) ? 1 : 0;
+    }
+    tf[w] = (uint16_t)id;
+    cnt[w] = c;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_minhold(const double* __restrict__ levels,
+                                                  const TomatisStream* __restrict__ st,
+                                                  const double* __restrict__ tlh,
+                                                  double target, double hyst, int mh, int xf,
+                                                  int alpha_adaptive, uint16_t* __restrict__ ws_tf,
+                                                  int32_t* __restrict__ ws_cnt,
+                                                  const int64_t* __restrict__ ws_off,
+                                                  double* __restrict__ t_out,
+                                                  uint8_t* __restrict__ states,
+                                                  uint16_t* __restrict__ rows,
+                                                  double* __restrict__ alpha) {
+  const int s = blockIdx.x;
+  const TomatisStream S = st[s];
+  const int64_t F = S.n_frames;
+  const double* lv = levels + S.frame_base;
+  uint16_t* tf = ws_tf + ws_off[s];
+  int32_t* cnt = ws_cnt + ws_off[s];
+  const int ns = 2 * (mh + 1);
+  const int nseg = (int)((F + kMhSeg - 1) / kMhSeg);
+  const int init_id = mh;  // C1, since = mh
+  __shared__ double sh_T;
+  __shared__ int sh_done;
+  __shared__ int sh_count;
+  double t_low = tlh[3 * s + 0], t_high = tlh[3 * s + 1];
+  double best_T = tlh[3 * s + 2], best_diff = 1.0;
+  const bool have_valid = !(t_low != t_low);
+  if (F > 0 && have_valid) {
+    for (int it = 0; it < 30; ++it) {
+      const double t_mid = (t_low + t_high) / 2;
+      const double ton = t_mid + hyst / 2, toff = t_mid - hyst / 2;
+      mh_simulate(lv, F, ton, toff, mh, tf, cnt);
+      __threadfence_block();
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        int id = init_id, c = 0;
+        for (int g = 0; g < nseg; ++g) {
+          c += cnt[(int64_t)g * ns + id];
+          id = tf[(int64_t)g * ns + id];
+        }
+        sh_count = c;
+      }
+      __syncthreads();
+      const double c2 = (double)sh_count / (double)F;
+      const double diff = fabs(c2 - target);
+      if (diff < best_diff) {
+        best_diff = diff;
+        best_T = t_mid;
+      }
+      if (diff < 0.01) break;
+      if (c2 < target) t_high = t_mid;
+      else t_low = t_mid;
+      __syncthreads();
+    }
+  }
+  if (threadIdx.x == 0) {
+    sh_T = best_T;
+    if (t_out) t_out[s] = best_T;
+  }
+  __syncthreads();
+  const double T = sh_T;
+  const double ton = T + hyst / 2, toff = T - hyst / 2;
+  // final states: sequential per segment starts, then parallel per segment
+  mh_simulate(lv, F, ton, toff, mh, tf, cnt);
+  __syncthreads();
+  __shared__ uint16_t seg_start[4096];
+  if (threadIdx.x == 0) {
+    int id = init_id;
+    for (int g = 0; g < nseg; ++g) {
+      if (g < 4096) seg_start[g] = (uint16_t)id;
+      id = tf[(int64_t)g * ns + id];
+    }
+  }
+  __syncthreads();
+  for (int g = threadIdx.x; g < nseg; g += blockDim.x) {
+    int id = (g < 4096) ? seg_start[g] : init_id;
+    const int64_t k0 = (int64_t)g * kMhSeg;
+    const int nf = (int)min<int64_t>(kMhSeg, F - k0);
+    for (int i = 0; i < nf; ++i) {
+      id = mh_step(id, lv[k0 + i], ton, toff, mh);
+      states[S.frame_base + k0 + i] = (id > mh) ? 2 : 1;
+    }
+  }
+  __syncthreads();
+  // alpha (process_tomatis_adaptive.py:253-265), sequential
+  if (threadIdx.x == 0 && F > 0) {
+    const double step = xf > 0 ? 1.0 / xf : 1.0;
+    const int xfe = xf > 0 ? xf : 1;
+    double a = states[S.frame_base] == 2 ? 1.0 : 0.0;
+    for (int64_t k = 0; k < F; ++k) {
+      const int64_t f = S.frame_base + k;
+      if (k > 0) a = alpha_step(a, states[f] == 2 ? 1.0 : 0.0, step);
+      if (alpha) alpha[f] = a;
+      if (rows) rows[f] = (uint16_t)(2 + (int)rint(a * xfe));
+    }
+  }
+  (void)alpha_adaptive;
+}
+
+// ===========================================================================
+// Fused STFT -> gain -> ISTFT -> OLA -> normalise (register OLA, hop % P == 0)
+// ===========================================================================
+struct MainArgs {
+  const float* x;
+  float* y;
+  const float* gains;
+  const uint16_t* rows;
+  uint32_t* peaks;
+  const TomatisStream* st;
+  const Run* runs;
+  const float* win;     // [N]
+  const float* win2;    // [N] win*win (f32)
+  const cf* twN;        // [32][P]
+  const cf* twP;        // [P]
+  const float* winv;    // [hop] 1/(interior wsum) (already normalisation-rule applied)
+  cf* scratch;          // generic path: [frames][N]
+  int n_runs, hop, n_bins, ch, norm_mode, rmax;
+  float inv_n;
+};
+
+__device__ __forceinline__ float norm_den(float w, int mode) {
+  return mode == TOMATIS_NORM_MAX ? fmaxf(w, 1e-8f) : (w + kEps32);
+}
+
+// wsum at position p, frames in ascending order (bit-exact with the reference's w_buf)
+__device__ float wsum_at(int64_t p, const TomatisStream& S, int hop, int N, const float* win2) {
+  const int64_t rel = p - S.first_start;
+  int64_t jhi = floordiv(rel, hop);
+  if (jhi > S.n_frames - 1) jhi = S.n_frames - 1;
+  int64_t jlo = floordiv(rel - N, hop) + 1;
+  if (jlo < 0) jlo = 0;
+  float w = 0.f;
+  for (int64_t j = jlo; j <= jhi; ++j) w = w + win2[rel - j * hop];
+  return w;
+}
+
+__device__ __forceinline__ int chunk_of(int64_t p, const TomatisStream& S) {
+  if (S.n_chunks <= 1 || p < S.chunk_first) return 0;
+  const int64_t c = 1 + (p - S.chunk_first) / S.chunk_len;
+  return (int)min<int64_t>(c, S.n_chunks - 1);
+}
+
+template <int P>
+__device__ __forceinline__ void flush_peak(float& pk, int cid, const TomatisStream& S,
+                                           uint32_t* peaks, int L) {
+  const float m = wave_max(pk);  // P > 64: each wave flushes its partial max
+  if ((L & 63) == 0 && cid >= 0 && m > 0.f) atomicMax(peaks + S.chunk_base + cid, __float_as_uint(m));
+  pk = 0.f;
+}
+
+template <int P, int SH, bool GENERIC>
+__global__ __launch_bounds__(256) void k_stft_ola(MainArgs A) {
+  using G = FftGeo<P>;
+  constexpr int N = G::N;
+  constexpr int NSEQ = 256 / P;
+  __shared__ cf s_twN[32 * P];
+  __shared__ cf s_twP[P];
+  __shared__ float s_win[N];
+  __shared__ cf s_buf[NSEQ][G::BUF];
+  for (int i = threadIdx.x; i < 32 * P; i += 256) s_twN[i] = A.twN[i];
+  for (int i = threadIdx.x; i < P; i += 256) s_twP[i] = A.twP[i];
+  for (int i = threadIdx.x; i < N; i += 256) s_win[i] = A.win[i];
+  __syncthreads();
+
+  const int seq = threadIdx.x / P, L = threadIdx.x % P;
+  const int run_id = blockIdx.x * NSEQ + seq;
+  // all sequences of the block iterate the same number of times when P > 64
+  Run R{0, 0, 0, 0};
+  bool valid = run_id < A.n_runs;
+  if (valid) R = A.runs[run_id];
+  if constexpr (P <= 64) {
+    if (!valid) return;
+  }
+  const TomatisStream S = A.st[R.s];
+  const int hop = A.hop;
+  const int64_t kfirst = max<int64_t>(0, R.ka - (A.rmax - 1));
+  int64_t nit = valid ? (R.kb - kfirst) : 0;
+  if constexpr (P > 64) {
+    // block-uniform trip count
+    __shared__ int64_t s_nit[NSEQ];
+    if (L == 0) s_nit[seq] = nit;
+    __syncthreads();
+    int64_t m = 0;
+    for (int i = 0; i < NSEQ; ++i) m = max(m, s_nit[i]);
+    nit = m;
+  }
+  cf* buf = s_buf[seq];
+  const float* xs = A.x + S.in_off;
+  float* ys = A.y + S.out_off;
+  const int64_t out_end = S.out_begin + S.out_len;
+  const float oscale = S.out_scale;
+  const float iscale = S.in_scale;
+
+  // per-lane interior 1/wsum for the emitted offsets m = L + P*i, i < SH
+  float winv[GENERIC ? 1 : SH];
+  if constexpr (!GENERIC) {
+#pragma unroll
+    for (int i = 0; i < SH; ++i) winv[i] = A.winv[L + P * i];
+  }
+  // zeros before frame 0 (adaptive: first frame starts after the output start)
+  if (valid && R.ka == 0 && S.first_start > S.out_begin) {
+    for (int64_t p = S.out_begin + L; p < min(S.first_start, out_end); p += P) {
+      const int64_t o = (p - S.out_begin) * A.ch;
+      if (A.ch == 2) *reinterpret_cast<float2*>(ys + o) = make_float2(0.f, 0.f);
+      else ys[o] = 0.f;
+    }
+  }
+
+  cf acc[GENERIC ? 1 : (32 - SH)];
+  if constexpr (!GENERIC) {
+#pragma unroll
+    for (int i = 0; i < 32 - SH; ++i) acc[i] = {0.f, 0.f};
+  }
+  float pk = 0.f;
+  int cid = -1;
+
+  for (int64_t it = 0; it < nit; ++it) {
+    const int64_t k = kfirst + it;
+    const bool live = valid && (k < R.kb);
+    const int64_t s_k = S.first_start + k * hop;
+    cf v[32];
+    // ---- load + analysis window ----
+    const bool interior = (s_k >= 0) && (s_k + N <= S.n);
+#pragma unroll
+    for (int n2 = 0; n2 < 32; ++n2) {
+      const int64_t p = s_k + L + P * n2;
+      cf z = {0.f, 0.f};
+      if (live && (interior || (p >= 0 && p < S.n))) {
+        if (A.ch == 2) {
+          const float2 t = *reinterpret_cast<const float2*>(xs + 2 * p);
+          z = {t.x * iscale, t.y * iscale};
+        } else {
+          z = {xs[p] * iscale, 0.f};
+        }
+      }
+      const float w = s_win[L + P * n2];
+      v[n2] = {z.x * w, z.y * w};
+    }
+    fft_fwd<P>(v, L, s_twN, s_twP, buf);
+    // ---- gain row (real, even) and 1/N ----
+    {
+      const uint16_t row = live ? A.rows[S.frame_base + k] : 0;
+      const float* g = A.gains + (int64_t)row * A.n_bins;
+#pragma unroll
+      for (int i = 0; i < 32; ++i) {
+        int b = fft_bin<P>(L, i);
+        b = (b <= N / 2) ? b : N - b;
+        const float gg = g[b] * A.inv_n;
+        v[i] = cscale(v[i], gg);
+      }
+    }
+    fft_inv<P>(v, L, s_twN, s_twP, buf);
+    // ---- synthesis window ----
+#pragma unroll
+    for (int n2 = 0; n2 < 32; ++n2) v[n2] = cscale(v[n2], s_win[L + P * n2]);
+
+    if constexpr (GENERIC) {
+      if (live) {
+        cf* dst = A.scratch + (S.frame_base + k) * (int64_t)N;
+#pragma unroll
+        for (int n2 = 0; n2 < 32; ++n2) dst[L + P * n2] = v[n2];
+      }
+    } else {
+      // ---- register OLA: v[n2] += acc[n2] (positions s_k + L + P*n2) ----
+#pragma unroll
+      for (int i = 0; i < 32 - SH; ++i) v[i] = v[i] + acc[i];
+      const bool emit = live && (k >= R.ka);
+      const bool edge = (k < A.rmax - 1);
+      if (emit) {
+        const int c0 = chunk_of(s_k, S), c1 = chunk_of(s_k + hop - 1, S);
+        if (c0 != cid) {
+          flush_peak<P>(pk, cid, S, A.peaks, L);
+          cid = c0;
+        }
+        float pk1 = 0.f;
+#pragma unroll
+        for (int i = 0; i < SH; ++i) {
+          const int64_t p = s_k + L + P * i;
+          if (p >= S.out_begin && p < out_end) {
+            cf o;
+            if (!edge) {
+              o = cscale(v[i], winv[i]);
+            } else {
+              const float d = norm_den(wsum_at(p, S, hop, N, A.win2), A.norm_mode);
+              o = {v[i].x / d, v[i].y / d};
+            }
+            o = cscale(o, oscale);
+            const int64_t oi = (p - S.out_begin) * A.ch;
+            if (A.ch == 2) *reinterpret_cast<float2*>(ys + oi) = make_float2(o.x, o.y);
+            else ys[oi] = o.x;
+            const float mag = (A.ch == 2) ? fmaxf(fabsf(o.x), fabsf(o.y)) : fabsf(o.x);
+            if (c0 == c1 || chunk_of(p, S) == c0) pk = fmaxf(pk, mag);
+            else pk1 = fmaxf(pk1, mag);
+          }
+        }
+        if (c1 != c0) {
+          flush_peak<P>(pk, cid, S, A.peaks, L);
+          cid = c1;
+          pk = pk1;
+        }
+        // tail of the stream: positions after the last frame's first hop
+        if (R.last && k == R.kb - 1) {
+#pragma unroll
+          for (int i = SH; i < 32; ++i) {
+            const int64_t p = s_k + L + P * i;
+            if (p >= S.out_begin && p < out_end) {
+              const float d = norm_den(wsum_at(p, S, hop, N, A.win2), A.norm_mode);
+              cf o = {v[i].x / d, v[i].y / d};
+              o = cscale(o, oscale);
+              const int64_t oi = (p - S.out_begin) * A.ch;
+              if (A.ch == 2) *reinterpret_cast<float2*>(ys + oi) = make_float2(o.x, o.y);
+              else ys[oi] = o.x;
+              const float mag = (A.ch == 2) ? fmaxf(fabsf(o.x), fabsf(o.y)) : fabsf(o.x);
+              const int c = chunk_of(p, S);
+              if (c == cid) pk = fmaxf(pk, mag);
+            }
+          }
+        }
+      }
+      // ---- shift the accumulator by one hop ----
+#pragma unroll
+      for (int i = 0; i < 32 - SH; ++i) acc[i] = v[i + SH];
+    }
+  }
+  if constexpr (!GENERIC) {
+    if (valid) flush_peak<P>(pk, cid, S, A.peaks, L);
+  }
+}
+
+// generic-hop OLA gather: one thread per output position (frame order preserved)
+__global__ __launch_bounds__(256) void k_ola_gather(MainArgs A, int n_streams,
+                                                    const int64_t* __restrict__ pos_base,
+                                                    int64_t total, int N) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  // stream lookup (binary search over position prefix)
+  int lo = 0, hi = n_streams - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) / 2;
+    if (pos_base[mid] <= t) lo = mid;
+    else hi = mid - 1;
+  }
+  const TomatisStream S = A.st[lo];
+  const int64_t p = S.out_begin + (t - pos_base[lo]);
+  const int hop = A.hop;
+  const int64_t rel = p - S.first_start;
+  int64_t jhi = floordiv(rel, hop);
+  if (jhi > S.n_frames - 1) jhi = S.n_frames - 1;
+  int64_t jlo = floordiv(rel - N, hop) + 1;
+  if (jlo < 0) jlo = 0;
+  float w = 0.f;
+  cf acc = {0.f, 0.f};
+  for (int64_t j = jlo; j <= jhi; ++j) {
+    const int off = (int)(rel - j * hop);
+    acc = acc + A.scratch[(S.frame_base + j) * (int64_t)N + off];
+    w = w + A.win2[off];
+  }
+  const float d = norm_den(w, A.norm_mode);
+  cf o = {acc.x / d, acc.y / d};
+  o = cscale(o, S.out_scale);
+  float* ys = A.y + S.out_off;
+  const int64_t oi = (p - S.out_begin) * A.ch;
+  if (A.ch == 2) *reinterpret_cast<float2*>(ys + oi) = make_float2(o.x, o.y);
+  else ys[oi] = o.x;
+  const float mag = (A.ch == 2) ? fmaxf(fabsf(o.x), fabsf(o.y)) : fabsf(o.x);
+  if (mag > 0.f) atomicMax(A.peaks + S.chunk_base + chunk_of(p, S), __float_as_uint(mag));
+}
+
+// ===========================================================================
+// limiter fix-up, absmax, scale, synth
+// ===========================================================================
+struct ChunkDesc {
+  int32_t s, c;
+  int64_t p0, p1;  // output-relative sample range [p0, p1)
+};
+
+__global__ __launch_bounds__(256) void k_limiter(float* __restrict__ y,
+                                                 const TomatisStream* __restrict__ st,
+                                                 const ChunkDesc* __restrict__ chunks,
+                                                 const uint32_t* __restrict__ peaks, float limit,
+                                                 int ch) {
+  const ChunkDesc C = chunks[blockIdx.y];
+  const TomatisStream S = st[C.s];
+  const float peak = __uint_as_float(peaks[S.chunk_base + C.c]);
+  if (!(peak > limit)) return;
+  const float sc = limit / peak;
+  const int64_t n = (C.p1 - C.p0) * ch;
+  float* base = y + S.out_off + C.p0 * ch;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    base[i] = base[i] * sc;
+}
+
+__global__ __launch_bounds__(256) void k_absmax(const float* __restrict__ x, int64_t n,
+                                                uint32_t* __restrict__ out) {
+  float m = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    m = fmaxf(m, fabsf(x[i]));
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0 && m > 0.f) atomicMax(out, __float_as_uint(m));
+}
+
+__global__ __launch_bounds__(256) void k_scale_copy(const float* __restrict__ x,
+                                                    float* __restrict__ y, int64_t n, float s) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = x[i] * s;
+}
+
+__device__ __forceinline__ uint32_t lowbias32(uint32_t v) {
+  v ^= v >> 16;
+  v *= 0x7FEB352Du;
+  v ^= v >> 15;
+  v *= 0x846CA68Bu;
+  v ^= v >> 16;
+  return v;
+}
+
+__global__ __launch_bounds__(256) void k_synth(float* __restrict__ x, int64_t n, int ch, int sr,
+                                               uint32_t seed, int64_t start) {
+  const uint32_t base = (uint32_t)((uint64_t)seed * 4u + 0x1234567u);
+  uint32_t key[4];
+  for (int j = 0; j < 4; ++j) key[j] = lowbias32(base + (uint32_t)j * 0x9E3779B9u);
+  const int64_t period = 3LL * sr, half = period / 2;
+  const int64_t ramp = max(1, sr / 100);
+  const float LOUD = 0.1f, QUIET = 0.001f;
+  const float d = QUIET - LOUD;
+  const int64_t total = n * ch;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t smp = start + e / ch;
+    const uint64_t eg = (uint64_t)(smp * ch + (e % ch));
+    const uint32_t lo = (uint32_t)eg, hi = (uint32_t)(eg >> 32);
+    float u[4];
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t v = lowbias32(lo ^ lowbias32(hi + key[j]));
+      u[j] = (float)(v >> 8) * (1.0f / 16777216.0f);
+    }
+    const float g = (((u[0] + u[1]) + (u[2] + u[3])) - 2.0f) * 1.7320508f;
+    const int64_t ph = smp % period;
+    float amp = ph < half ? QUIET : LOUD;
+    if (ph < ramp) amp = LOUD + d * ((float)ph / (float)ramp);
+    else if (ph >= half && ph < half + ramp) amp = QUIET + (-d) * ((float)(ph - half) / (float)ramp);
+    float v = g * amp;
+    v = fminf(fmaxf(v, -1.0f), 1.0f);
+    x[e] = v;
+  }
+}
+
+}  // namespace
+
+
+// ===========================================================================
+// Host side: plan + C ABI
+// ===========================================================================
+struct tomatis_plan_s {
+  TomatisPlanDesc d{};
+  int32_t n_streams = 0;
+  int64_t total_frames = 0;
+  int32_t total_chunks = 0;
+  int P = 0, SH = 0, rmax = 1;
+  bool generic = false;
+  std::vector<TomatisStream> hs;
+  int lvl_nf = 0;
+  // device
+  TomatisStream* st = nullptr;
+  Run* runs = nullptr;
+  int n_runs = 0;
+  LvlBlock* lblocks = nullptr;
+  int n_lblocks = 0;
+  GateSeg* segs = nullptr;
+  int n_segs = 0;
+  int32_t* seg_first = nullptr;
+  int32_t* seg_count = nullptr;
+  uint16_t* tf = nullptr;
+  uint16_t* seg_start = nullptr;
+  float* win = nullptr;
+  float* win2 = nullptr;
+  float* winv = nullptr;
+  cf* twN = nullptr;
+  cf* twP = nullptr;
+  cf* scratch = nullptr;
+  int64_t* pos_base = nullptr;
+  int64_t total_out = 0;
+  ChunkDesc* chunks = nullptr;
+  int n_chunkdesc = 0;
+  int64_t max_chunk = 0;
+  uint16_t* mh_tf = nullptr;
+  int32_t* mh_cnt = nullptr;
+  int64_t* mh_off = nullptr;
+};
+
+namespace {
+
+int hipfail(hipError_t e) { return e == hipSuccess ? TOMATIS_OK : TOMATIS_E_HIP; }
+
+template <typename T>
+int dalloc_copy(T** dst, const std::vector<T>& v) {
+  *dst = nullptr;
+  if (v.empty()) return TOMATIS_OK;
+  if (hipMalloc(reinterpret_cast<void**>(dst), v.size() * sizeof(T)) != hipSuccess) {
+    *dst = nullptr;
+    return TOMATIS_E_NOMEM;
+  }
+  return hipfail(hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+}
+
+void dfree(void* p) {
+  if (p) (void)hipFree(p);
+}
+
+int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+
+int launch_check() { return hipfail(hipGetLastError()); }
+
+template <int P, int SH, bool GEN>
+void launch_main(const MainArgs& A, int nseq_blocks, hipStream_t s) {
+  hipLaunchKernelGGL((k_stft_ola<P, SH, GEN>), dim3(nseq_blocks), dim3(256), 0, s, A);
+}
+
+}  // namespace
+
+extern "C" {
+
+int tomatis_abi_version(void) { return TOMATIS_ABI_VERSION; }
+
+const char* tomatis_status_string(int s) {
+  switch (s) {
+    case TOMATIS_OK: return "ok";
+    case TOMATIS_E_ARG: return "invalid argument";
+    case TOMATIS_E_UNSUPPORTED: return "configuration not supported by the gfx950 kernels";
+    case TOMATIS_E_HIP: return "HIP runtime error";
+    case TOMATIS_E_NOMEM: return "device allocation failed";
+    default: return "unknown status";
+  }
+}
+
+int tomatis_plan_destroy(tomatis_plan_t p) {
+  if (!p) return TOMATIS_OK;
+  void* ptrs[] = {p->st, p->runs, p->lblocks, p->segs, p->seg_first, p->seg_count, p->tf,
+                  p->seg_start, p->win, p->win2, p->winv, p->twN, p->twP, p->scratch,
+                  p->pos_base, p->chunks, p->mh_tf, p->mh_cnt, p->mh_off};
+  for (void* q : ptrs) dfree(q);
+  delete p;
+  return TOMATIS_OK;
+}
+
+int64_t tomatis_plan_total_frames(tomatis_plan_t p) { return p ? p->total_frames : -1; }
+int32_t tomatis_plan_total_chunks(tomatis_plan_t p) { return p ? p->total_chunks : -1; }
+
+static int plan_build(tomatis_plan_s* p, const float* window) {
+  const TomatisPlanDesc& d = p->d;
+  const int N = d.n_fft, hop = d.hop, P = p->P;
+  int rc;
+  const int ns = p->n_streams;
+  // --- stream table ---
+  if ((rc = dalloc_copy(&p->st, p->hs))) return rc;
+  // --- main-kernel runs ---
+  const int64_t tf_total = std::max<int64_t>(1, p->total_frames);
+  int T = env_int("TOMATIS_RUN_FRAMES", 0);
+  if (T <= 0) {
+    const int64_t target = (P == 64) ? 8192 : 4096;
+    T = (int)std::max<int64_t>(48, (tf_total + target - 1) / target);
+  }
+  std::vector<Run> runs;
+  for (int s = 0; s < ns; ++s) {
+    const int64_t F = p->hs[s].n_frames;
+    for (int64_t a = 0; a < F; a += T) {
+      Run r;
+      r.s = s;
+      r.ka = a;
+      r.kb = std::min<int64_t>(F, a + T);
+      r.last = (r.kb == F) ? 1 : 0;
+      runs.push_back(r);
+    }
+  }
+  p->n_runs = (int)runs.size();
+  if ((rc = dalloc_copy(&p->runs, runs))) return rc;
+  // --- levels blocks ---
+  {
+    const int arr_f32 = kLevelLds + 256;  // matches k_levels<float> LDS
+    const int cap = (arr_f32 * 128) / 132 - 8;
+    p->lvl_nf = std::max(1, (cap - N) / hop + 1);
+    const int nleaf = N >> 7;
+    p->lvl_nf = std::min(p->lvl_nf, 1024 / nleaf);
+    std::vector<LvlBlock> lb;
+    for (int s = 0; s < ns; ++s) {
+      const int64_t F = p->hs[s].n_frames;
+      for (int64_t a = 0; a < F; a += p->lvl_nf) {
+        LvlBlock b;
+        b.s = s;
+        b.k0 = a;
+        b.nf = (int)std::min<int64_t>(p->lvl_nf, F - a);
+        lb.push_back(b);
+      }
+    }
+    p->n_lblocks = (int)lb.size();
+    if ((rc = dalloc_copy(&p->lblocks, lb))) return rc;
+  }
+  // --- gate segments ---
+  {
+    std::vector<GateSeg> sg;
+    std::vector<int32_t> first(ns), count(ns);
+    for (int s = 0; s < ns; ++s) {
+      const int64_t F = p->hs[s].n_frames;
+      first[s] = (int32_t)sg.size();
+      for (int64_t a = 0; a < F; a += kSeg) {
+        GateSeg g;
+        g.s = s;
+        g.k0 = a;
+        g.nf = (int)std::min<int64_t>(kSeg, F - a);
+        sg.push_back(g);
+      }
+      count[s] = (int32_t)sg.size() - first[s];
+    }
+    p->n_segs = (int)sg.size();
+    if ((rc = dalloc_copy(&p->segs, sg))) return rc;
+    if ((rc = dalloc_copy(&p->seg_first, first))) return rc;
+    if ((rc = dalloc_copy(&p->seg_count, count))) return rc;
+    const int nstate = d.up_delay_frames + 2;
+    if (p->n_segs > 0) {
+      if (hipMalloc(reinterpret_cast<void**>(&p->tf), (size_t)p->n_segs * nstate * sizeof(uint16_t)))
+        return TOMATIS_E_NOMEM;
+      if (hipMalloc(reinterpret_cast<void**>(&p->seg_start), (size_t)p->n_segs * sizeof(uint16_t)))
+        return TOMATIS_E_NOMEM;
+    }
+  }
+  // --- tables ---
+  {
+    std::vector<float> w(window, window + N), w2(N);
+    for (int i = 0; i < N; ++i) w2[i] = w[i] * w[i];
+    std::vector<float> winv(hop);
+    for (int m = 0; m < hop; ++m) {
+      // frames covering an interior position with hop-offset m, ascending frame order
+      const int Rm = (N - m + hop - 1) / hop;
+      float acc = 0.f;
+      for (int j = Rm - 1; j >= 0; --j) acc = acc + w2[m + j * hop];
+      const float den = (d.norm_mode == TOMATIS_NORM_MAX) ? std::max(acc, 1e-8f) : (acc + 1e-12f);
+      winv[m] = 1.0f / den;
+    }
+    p->rmax = (N + hop - 1) / hop;
+    std::vector<cf> twN((size_t)32 * P), twP(P);
+    for (int k2 = 0; k2 < 32; ++k2)
+      for (int n1 = 0; n1 < P; ++n1) {
+        const double ang = -2.0 * M_PI * (double)((int64_t)n1 * k2 % N) / (double)N;
+        twN[(size_t)k2 * P + n1] = {(float)cos(ang), (float)sin(ang)};
+      }
+    for (int m = 0; m < P; ++m) {
+      const double ang = -2.0 * M_PI * (double)m / (double)P;
+      twP[m] = {(float)cos(ang), (float)sin(ang)};
+    }
+    if ((rc = dalloc_copy(&p->win, w))) return rc;
+    if ((rc = dalloc_copy(&p->win2, w2))) return rc;
+    if ((rc = dalloc_copy(&p->winv, winv))) return rc;
+    if ((rc = dalloc_copy(&p->twN, twN))) return rc;
+    if ((rc = dalloc_copy(&p->twP, twP))) return rc;
+  }
+  // --- limiter chunk descriptors, output prefix ---
+  {
+    std::vector<ChunkDesc> cd;
+    std::vector<int64_t> pb(ns);
+    int64_t tot = 0, mx = 0;
+    for (int s = 0; s < ns; ++s) {
+      const TomatisStream& S = p->hs[s];
+      pb[s] = tot;
+      tot += S.out_len;
+      const int64_t ob = S.out_begin, oe = S.out_begin + S.out_len;
+      for (int c = 0; c < S.n_chunks; ++c) {
+        int64_t b0 = (c == 0) ? INT64_MIN / 4 : S.chunk_first + (int64_t)(c - 1) * S.chunk_len;
+        int64_t b1 = (c == S.n_chunks - 1) ? INT64_MAX / 4 : S.chunk_first + (int64_t)c * S.chunk_len;
+        b0 = std::max(b0, ob);
+        b1 = std::min(b1, oe);
+        if (b1 <= b0) continue;
+        ChunkDesc C;
+        C.s = s;
+        C.c = c;
+        C.p0 = b0 - ob;
+        C.p1 = b1 - ob;
+        mx = std::max(mx, b1 - b0);
+        cd.push_back(C);
+      }
+    }
+    p->n_chunkdesc = (int)cd.size();
+    p->max_chunk = mx;
+    p->total_out = tot;
+    if ((rc = dalloc_copy(&p->chunks, cd))) return rc;
+    if ((rc = dalloc_copy(&p->pos_base, pb))) return rc;
+  }
+  // --- generic-hop scratch ---
+  if (p->generic && p->total_frames > 0) {
+    if (hipMalloc(reinterpret_cast<void**>(&p->scratch), (size_t)p->total_frames * N * sizeof(cf)))
+      return TOMATIS_E_NOMEM;
+  }
+  // --- min-hold workspace ---
+  if (d.min_hold_frames >= 0) {
+    const int nsm = 2 * (d.min_hold_frames + 1);
+    std::vector<int64_t> off(ns + 1, 0);
+    for (int s = 0; s < ns; ++s) {
+      const int64_t nseg = (p->hs[s].n_frames + kMhSeg - 1) / kMhSeg;
+      off[s + 1] = off[s] + nseg * nsm;
+    }
+    if ((rc = dalloc_copy(&p->mh_off, off))) return rc;
+    if (off[ns] > 0) {
+      if (hipMalloc(reinterpret_cast<void**>(&p->mh_tf), off[ns] * sizeof(uint16_t))) return TOMATIS_E_NOMEM;
+      if (hipMalloc(reinterpret_cast<void**>(&p->mh_cnt), off[ns] * sizeof(int32_t))) return TOMATIS_E_NOMEM;
+    }
+  }
+  return TOMATIS_OK;
+}
+
+int tomatis_plan_create(tomatis_plan_t* out, const TomatisPlanDesc* desc, const float* window,
+                        TomatisStream* streams, int32_t n_streams) {
+  if (!out || !desc || !window || (!streams && n_streams > 0) || n_streams < 0) return TOMATIS_E_ARG;
+  *out = nullptr;
+  const TomatisPlanDesc d = *desc;
+  if (d.n_fft != 2048 && d.n_fft != 4096) return TOMATIS_E_UNSUPPORTED;
+  if (d.ch < 1 || d.ch > 2) return TOMATIS_E_UNSUPPORTED;
+  if (d.hop < 1 || d.hop > d.n_fft) return TOMATIS_E_ARG;
+  if (d.up_delay_frames < 0 || d.up_delay_frames + 2 > kMaxGateStates) return TOMATIS_E_UNSUPPORTED;
+  if (d.min_hold_frames < 0 || 2 * (d.min_hold_frames + 1) > 65535) return TOMATIS_E_UNSUPPORTED;
+  if (d.norm_mode != TOMATIS_NORM_EPS && d.norm_mode != TOMATIS_NORM_MAX) return TOMATIS_E_ARG;
+  auto* p = new (std::nothrow) tomatis_plan_s();
+  if (!p) return TOMATIS_E_NOMEM;
+  p->d = d;
+  p->n_streams = n_streams;
+  const int N = d.n_fft, hop = d.hop;
+  p->P = N / 32;
+  p->SH = (hop % p->P == 0) ? hop / p->P : 0;
+  p->generic = !(p->SH == 4 || p->SH == 8 || p->SH == 16);
+  int64_t fb = 0;
+  int32_t cb = 0;
+  for (int i = 0; i < n_streams; ++i) {
+    TomatisStream& s = streams[i];
+    bool bad = s.n < 0 || s.n_frames < 0 || s.out_len < 0 || s.n_chunks < 1 ||
+               (s.n_chunks > 1 && s.chunk_len <= 0);
+    if (!bad && s.n_frames > 0 && s.out_begin + s.out_len > s.first_start + (s.n_frames - 1) * hop + N)
+      bad = true;  // output beyond the last frame end is never produced
+    if (!bad && s.n_frames == 0 && s.out_len > 0) bad = true;
+    if (bad) {
+      delete p;
+      return TOMATIS_E_ARG;
+    }
+    s.frame_base = fb;
+    s.chunk_base = cb;
+    fb += s.n_frames;
+    cb += s.n_chunks;
+  }
+  p->total_frames = fb;
+  p->total_chunks = cb;
+  p->hs.assign(streams, streams + n_streams);
+  const int rc = plan_build(p, window);
+  if (rc != TOMATIS_OK) {
+    tomatis_plan_destroy(p);
+    return rc;
+  }
+  *out = p;
+  return TOMATIS_OK;
+}
+
+int tomatis_plan_update_streams(tomatis_plan_t p, const TomatisStream* streams, void* hs) {
+  if (!p || !streams) return TOMATIS_E_ARG;
+  for (int i = 0; i < p->n_streams; ++i) {
+    TomatisStream s = streams[i];
+    s.frame_base = p->hs[i].frame_base;
+    s.chunk_base = p->hs[i].chunk_base;
+    p->hs[i] = s;
+  }
+  if (p->n_streams == 0) return TOMATIS_OK;
+  return hipfail(hipMemcpyAsync(p->st, p->hs.data(), p->hs.size() * sizeof(TomatisStream),
+                                hipMemcpyHostToDevice, (hipStream_t)hs));
+}
+
+int tomatis_levels(tomatis_plan_t p, const float* x, void* r_out, int32_t prec, void* hs) {
+  if (!p || !x || !r_out) return TOMATIS_E_ARG;
+  if (p->n_lblocks == 0) return TOMATIS_OK;
+  hipStream_t s = (hipStream_t)hs;
+  if (prec == TOMATIS_F32) {
+    hipLaunchKernelGGL((k_levels<float, true>), dim3(p->n_lblocks), dim3(256), 0, s, x, p->st,
+                       p->lblocks, p->d.n_fft, p->d.hop, p->d.ch, (float*)r_out);
+  } else if (prec == TOMATIS_F64) {
+    // f64 blocks hold half the frames: launch twice the blocks over half-size items
+    const int N = p->d.n_fft, hop = p->d.hop;
+    const int cap = ((kLevelLds / 2 + 256) * 128) / 132 - 8;
+    const int nf64 = std::max(1, (cap - N) / hop + 1);
+    if (nf64 < p->lvl_nf) {
+      // build a finer block list on the fly (small host work, cached per call)
+      std::vector<LvlBlock> lb;
+      for (int st = 0; st < p->n_streams; ++st) {
+        const int64_t F = p->hs[st].n_frames;
+        for (int64_t a = 0; a < F; a += nf64) {
+          LvlBlock b;
+          b.s = st;
+          b.k0 = a;
+          b.nf = (int)std::min<int64_t>(nf64, F - a);
+          lb.push_back(b);
+        }
+      }
+      LvlBlock* dlb = nullptr;
+      int rc = dalloc_copy(&dlb, lb);
+      if (rc) return rc;
+      hipLaunchKernelGGL((k_levels<double, true>), dim3((unsigned)lb.size()), dim3(256), 0, s, x,
+                         p->st, dlb, N, hop, p->d.ch, (double*)r_out);
+      rc = launch_check();
+      (void)hipStreamSynchronize(s);
+      dfree(dlb);
+      return rc;
+    }
+    hipLaunchKernelGGL((k_levels<double, true>), dim3(p->n_lblocks), dim3(256), 0, s, x, p->st,
+                       p->lblocks, p->d.n_fft, p->d.hop, p->d.ch, (double*)r_out);
+  } else {
+    return TOMATIS_E_ARG;
+  }
+  return launch_check();
+}
+
+int tomatis_gate_std(tomatis_plan_t p, const float* r, uint8_t* states, uint16_t* rows,
+                     double* alpha_out, void* hs) {
+  if (!p || !r || !states || !rows) return TOMATIS_E_ARG;
+  if (p->n_segs == 0) return TOMATIS_OK;
+  hipStream_t s = (hipStream_t)hs;
+  const int D = p->d.up_delay_frames;
+  hipLaunchKernelGGL(k_gate_tf, dim3((p->n_segs + 3) / 4), dim3(256), 0, s, r, p->st, p->segs,
+                     p->n_segs, D, p->tf);
+  hipLaunchKernelGGL(k_gate_chain, dim3((p->n_streams + 63) / 64), dim3(64), 0, s, p->st,
+                     p->n_streams, p->seg_first, p->seg_count, D + 2, p->tf, p->seg_start, 0);
+  const bool xf = p->d.alpha_mode == 1;
+  hipLaunchKernelGGL(k_gate_resolve, dim3((p->n_segs + 3) / 4), dim3(256), 0, s, r, p->st,
+                     p->segs, p->n_segs, D, p->seg_start, states, xf ? nullptr : rows);
+  if (xf) {
+    hipLaunchKernelGGL(k_alpha_xfade, dim3((p->n_streams + 63) / 64), dim3(64), 0, s, p->st,
+                       p->n_streams, states, p->d.xfade_frames, rows, alpha_out);
+  }
+  return launch_check();
+}
+
+int tomatis_minhold_bisect(tomatis_plan_t p, const double* levels, const double* tlh,
+                           double target_c2, double hyst_db, double* t_out, uint8_t* states,
+                           uint16_t* rows, double* alpha_out, void* hs) {
+  if (!p || !levels || !tlh || !states) return TOMATIS_E_ARG;
+  if (p->n_streams == 0) return TOMATIS_OK;
+  hipStream_t s = (hipStream_t)hs;
+  hipLaunchKernelGGL(k_minhold, dim3(p->n_streams), dim3(1024), 0, s, levels, p->st, tlh,
+                     target_c2, hyst_db, p->d.min_hold_frames, p->d.xfade_frames, 1, p->mh_tf,
+                     p->mh_cnt, p->mh_off, t_out, states, rows, alpha_out);
+  return launch_check();
+}
+
+int tomatis_stft_ola(tomatis_plan_t p, const float* x, const float* gains, int32_t n_rows,
+                     const uint16_t* rows, float* y, uint32_t* peaks, void* hs) {
+  if (!p || !x || !gains || !rows || !y || !peaks || n_rows < 1) return TOMATIS_E_ARG;
+  if (p->n_runs == 0) return TOMATIS_OK;
+  hipStream_t s = (hipStream_t)hs;
+  MainArgs A;
+  A.x = x;
+  A.y = y;
+  A.gains = gains;
+  A.rows = rows;
+  A.peaks = peaks;
+  A.st = p->st;
+  A.runs = p->runs;
+  A.win = p->win;
+  A.win2 = p->win2;
+  A.twN = p->twN;
+  A.twP = p->twP;
+  A.winv = p->winv;
+  A.scratch = p->scratch;
+  A.n_runs = p->n_runs;
+  A.hop = p->d.hop;
+  A.n_bins = p->d.n_fft / 2 + 1;
+  A.ch = p->d.ch;
+  A.norm_mode = p->d.norm_mode;
+  A.rmax = p->generic ? 1 : p->rmax;
+  A.inv_n = 1.0f / (float)p->d.n_fft;
+  const int nseq = 256 / p->P;
+  const int blocks = (p->n_runs + nseq - 1) / nseq;
+  if (p->P == 64) {
+    if (p->generic) launch_main<64, 1, true>(A, blocks, s);
+    else if (p->SH == 4) launch_main<64, 4, false>(A, blocks, s);
+    else if (p->SH == 8) launch_main<64, 8, false>(A, blocks, s);
+    else launch_main<64, 16, false>(A, blocks, s);
+  } else {
+    if (p->generic) launch_main<128, 1, true>(A, blocks, s);
+    else if (p->SH == 4) launch_main<128, 4, false>(A, blocks, s);
+    else if (p->SH == 8) launch_main<128, 8, false>(A, blocks, s);
+    else launch_main<128, 16, false>(A, blocks, s);
+  }
+  int rc = launch_check();
+  if (rc || !p->generic || p->total_out == 0) return rc;
+  const int64_t nb = (p->total_out + 255) / 256;
+  hipLaunchKernelGGL(k_ola_gather, dim3((unsigned)nb), dim3(256), 0, s, A, p->n_streams,
+                     p->pos_base, p->total_out, p->d.n_fft);
+  return launch_check();
+}
+
+int tomatis_apply_limiter(tomatis_plan_t p, float* y, const uint32_t* peaks, float limit, void* hs) {
+  if (!p || !y || !peaks) return TOMATIS_E_ARG;
+  if (p->n_chunkdesc == 0) return TOMATIS_OK;
+  const int64_t per = p->max_chunk * p->d.ch;
+  const unsigned gx = (unsigned)std::min<int64_t>(std::max<int64_t>(1, (per + 1023) / 1024), 4096);
+  hipLaunchKernelGGL(k_limiter, dim3(gx, p->n_chunkdesc), dim3(256), 0, (hipStream_t)hs, y, p->st,
+                     p->chunks, peaks, limit, p->d.ch);
+  return launch_check();
+}
+
+int tomatis_absmax(const float* x, int64_t n, uint32_t* out, void* hs) {
+  if (!x || !out || n < 0) return TOMATIS_E_ARG;
+  if (n == 0) return TOMATIS_OK;
+  const unsigned g = (unsigned)std::min<int64_t>(2048, (n + 1023) / 1024);
+  hipLaunchKernelGGL(k_absmax, dim3(g), dim3(256), 0, (hipStream_t)hs, x, n, out);
+  return launch_check();
+}
+
+int tomatis_scale_copy(const float* x, float* y, int64_t n, float scale, void* hs) {
+  if (!x || !y || n < 0) return TOMATIS_E_ARG;
+  if (n == 0) return TOMATIS_OK;
+  const unsigned g = (unsigned)std::min<int64_t>(4096, (n + 1023) / 1024);
+  hipLaunchKernelGGL(k_scale_copy, dim3(g), dim3(256), 0, (hipStream_t)hs, x, y, n, scale);
+  return launch_check();
+}
+
+int tomatis_synth_fill(float* x, int64_t n, int32_t ch, int32_t sr, uint32_t seed, int64_t start,
+                       void* hs) {
+  if (!x || n < 0 || ch < 1 || sr < 1) return TOMATIS_E_ARG;
+  if (n == 0) return TOMATIS_OK;
+  const unsigned g = (unsigned)std::min<int64_t>(8192, (n * ch + 1023) / 1024);
+  hipLaunchKernelGGL(k_synth, dim3(g), dim3(256), 0, (hipStream_t)hs, x, n, ch, sr, seed, start);
+  return launch_check();
+}
+
+}  // extern "C"

@@ -1,0 +1,587 @@
+"""Device orchestration of the STFT-gate-OLA hot path on MI355X.
+
+A *stream set* is a batch of equal-format PCM streams (same sr, ch) resident
+in one flat float32 HBM buffer (interleaved ``[n][ch]`` per stream).  A
+pipeline builds one ``tomatis_plan`` for the set (work decomposition, tables)
+and allocates every per-frame / per-chunk buffer up front, so ``run()`` only
+launches kernels on the current stream (no host sync for the standard, xfade
+and EQ paths; the adaptive path syncs once for the level percentiles).
+
+Reference behaviour reproduced per mode (file:line):
+  standard  src/process_tomatis.py:160-457
+  xfade     src/process_tomatis_xfade.py:55-341
+  adaptive  src/process_tomatis_adaptive.py:157-351
+  layer2    src/layer2_apply_eq.py:66-233
+  layer2b   src/layer2b_apply_residual_eq.py:57-160 (+ _safe.py)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import dsp
+from ._lib import (F32, F64, NORM_EPS, NORM_MAX, TomatisPlanDesc, TomatisStream, check, lib,
+                   ptr, stream_handle)
+
+PEAK_LIMIT = 0.999
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        raise RuntimeError("tomatis_audio_processor_amd needs a ROCm GPU (MI355X); "
+                           "torch.cuda.is_available() is False and there is no CPU fallback")
+    return torch
+
+
+@dataclass
+class StreamSet:
+    """Equal-format streams in one flat device buffer."""
+    x: object                 # torch.float32 cuda tensor (flat)
+    offs: List[int]           # float offset of each stream's sample 0
+    lens: List[int]           # samples per channel
+    ch: int
+    sr: int
+
+    @classmethod
+    def from_arrays(cls, arrays: Sequence[np.ndarray], sr: int, device="cuda"):
+        torch = _torch()
+        arrays = [np.ascontiguousarray(np.asarray(a, np.float32).reshape(len(a), -1))
+                  for a in arrays]
+        ch = arrays[0].shape[1]
+        if any(a.shape[1] != ch for a in arrays):
+            raise ValueError("all streams of a set must have the same channel count")
+        offs, tot = [], 0
+        for a in arrays:
+            offs.append(tot)
+            tot += a.size
+        flat = np.concatenate([a.reshape(-1) for a in arrays]) if arrays else np.zeros(0, np.float32)
+        x = torch.from_numpy(flat).to(device)
+        return cls(x=x, offs=offs, lens=[a.shape[0] for a in arrays], ch=ch, sr=sr)
+
+    @classmethod
+    def synthetic(cls, n_streams: int, n: int, ch: int, sr: int, seed0: int = 1000,
+                  device="cuda"):
+        """Seeded synthetic streams generated on the device (synth.py twin)."""
+        torch = _torch()
+        x = torch.empty(n_streams * n * ch, dtype=torch.float32, device=device)
+        L = lib()
+        hs = stream_handle()
+        for i in range(n_streams):
+            sub = x[i * n * ch:(i + 1) * n * ch]
+            check(L.tomatis_synth_fill(ptr(sub), n, ch, sr, seed0 + i, 0, hs), "synth_fill")
+        return cls(x=x, offs=[i * n * ch for i in range(n_streams)], lens=[n] * n_streams,
+                   ch=ch, sr=sr)
+
+    @property
+    def n_streams(self):
+        return len(self.lens)
+
+
+class Plan:
+    """Owns a ``tomatis_plan_t``."""
+
+    def __init__(self, desc: TomatisPlanDesc, window: np.ndarray, streams: List[TomatisStream]):
+        L = lib()
+        self.L = L
+        self.n = len(streams)
+        self.streams = (TomatisStream * max(1, self.n))(*streams)
+        win = np.ascontiguousarray(window, np.float32)
+        self._win = win
+        h = C.c_void_p()
+        check(L.tomatis_plan_create(C.byref(h), C.byref(desc),
+                                    win.ctypes.data_as(C.POINTER(C.c_float)),
+                                    self.streams, self.n), "plan_create")
+        self.h = h
+        self.total_frames = int(L.tomatis_plan_total_frames(h))
+        self.total_chunks = int(L.tomatis_plan_total_chunks(h))
+
+    def update(self):
+        check(self.L.tomatis_plan_update_streams(self.h, self.streams, stream_handle()),
+              "plan_update_streams")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.tomatis_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _set_gate(st: TomatisStream, Ton: float, Toff: float):
+    on, oe, off, fe = dsp.gate_bits(Ton, Toff)
+    st.on_bits, st.off_bits = on, off
+    st.n_on_exc, st.n_off_exc = len(oe), len(fe)
+    for i, b in enumerate(oe):
+        st.on_exc[i] = b
+    for i, b in enumerate(fe):
+        st.off_exc[i] = b
+    st.t_on, st.t_off = Ton, Toff
+
+
+@dataclass
+class Result:
+    y: object                       # flat float32 device tensor of all outputs
+    out_offs: List[int]
+    out_lens: List[int]
+    ch: int
+    frame_base: List[int]
+    n_frames: List[int]
+    first_start: List[int]
+    hop: int
+    states: object = None           # device uint8 per frame
+    r: object = None                # device f32 (or f64) per frame
+    alpha: object = None            # device f64 per frame
+    chunk_peaks: object = None      # device uint32 bits per chunk
+    chunk_base: List[int] = field(default_factory=list)
+    n_chunks: List[int] = field(default_factory=list)
+    extra: dict = field(default_factory=dict)
+
+    def output(self, i: int) -> np.ndarray:
+        a = self.out_offs[i]
+        n = self.out_lens[i] * self.ch
+        return self.y[a:a + n].cpu().numpy().reshape(self.out_lens[i], self.ch)
+
+    def stream_states(self, i: int) -> np.ndarray:
+        a = self.frame_base[i]
+        return self.states[a:a + self.n_frames[i]].cpu().numpy()
+
+    def stream_r(self, i: int) -> np.ndarray:
+        a = self.frame_base[i]
+        return self.r[a:a + self.n_frames[i]].cpu().numpy()
+
+    def stream_alpha(self, i: int) -> np.ndarray:
+        a = self.frame_base[i]
+        return self.alpha[a:a + self.n_frames[i]].cpu().numpy()
+
+    def stream_peaks(self, i: int) -> np.ndarray:
+        a = self.chunk_base[i]
+        b = self.chunk_peaks[a:a + self.n_chunks[i]].cpu().numpy().astype(np.uint32)
+        return b.view(np.float32)
+
+
+def _alloc_out(torch, lens, ch, device):
+    offs, tot = [], 0
+    for n in lens:
+        offs.append(tot)
+        tot += n * ch
+    return torch.empty(max(1, tot), dtype=torch.float32, device=device), offs
+
+
+def _check_fft(n_fft, hop, ch):
+    if n_fft not in (2048, 4096):
+        raise ValueError(f"n_fft={n_fft}: the gfx950 kernels are built for n_fft 2048 and 4096")
+    if not (1 <= hop <= n_fft):
+        raise ValueError(f"hop={hop} must be in [1, n_fft]")
+    if ch not in (1, 2):
+        raise ValueError(f"{ch} channels: the gfx950 kernels handle mono and stereo")
+
+
+# ---------------------------------------------------------------------------
+# standard / xfade
+# ---------------------------------------------------------------------------
+
+class GatePipeline:
+    """Standard (process_tomatis) or xfade (process_tomatis_xfade) processing."""
+
+    def __init__(self, ss: StreamSet, *, gate_ui=50, gate_mode="log_percent",
+                 dynamic_range=80.0, gate_scale=1.0, gate_offset=-100, hysteresis_db=3.0,
+                 fc=1000.0, slope=12.0, c1_low=15.0, c1_high=-15.0, c2_low=-15.0,
+                 c2_high=15.0, up_delay_ms=250.0, n_fft=4096, hop=2048,
+                 output_gain_db=0.0, xfade_ms=None):
+        torch = _torch()
+        _check_fft(n_fft, hop, ss.ch)
+        self.ss, self.n_fft, self.hop = ss, n_fft, hop
+        sr = ss.sr
+        freqs = np.fft.rfftfreq(n_fft, d=1.0 / sr)
+        g1_db = dsp.build_tilt_gain_db(freqs, fc, slope, c1_low, c1_high)
+        g2_db = dsp.build_tilt_gain_db(freqs, fc, slope, c2_low, c2_high)
+        g1, g2 = dsp.db_to_lin(g1_db), dsp.db_to_lin(g2_db)
+        xf = 0
+        rows = [g1, g2]
+        self.xfade = xfade_ms is not None
+        if self.xfade:
+            frame_ms = hop / sr * 1000.0
+            xf = max(1, int(np.ceil(xfade_ms / frame_ms))) if xfade_ms > 0 else 0
+            for a in _alpha_lattice(xf):
+                rows.append(dsp.db_to_lin((1 - a) * g1_db + a * g2_db))
+            T = dsp.gate_ui_to_dbfs(gate_ui, gate_scale, gate_offset)
+        elif gate_mode == "log_percent":
+            T = dsp.gate_ui_to_dbfs_log_percent(gate_ui, dynamic_range)
+        else:
+            T = dsp.gate_ui_to_dbfs(gate_ui, gate_scale, gate_offset)
+        self.T = T
+        self.Ton, self.Toff = T + hysteresis_db / 2.0, T - hysteresis_db / 2.0
+        D = int(sr * up_delay_ms / 1000.0)
+        self.up_delay_samples = D
+        Dk = max(0, -(-D // hop))
+        self.xf = xf
+        out_scale = np.float32(10.0 ** (output_gain_db / 20.0)) if (
+            output_gain_db != 0.0 and not self.xfade) else np.float32(1.0)
+        streams = []
+        self.bounds = []
+        for off, N in zip(ss.offs, ss.lens):
+            pad, pe, F, s0 = dsp.std_schedule(N, n_fft, hop)
+            b = dsp.std_flush_bounds(N, n_fft, hop)
+            self.bounds.append(b)
+            st = TomatisStream()
+            st.in_off, st.n, st.first_start, st.n_frames = off, N, s0, F
+            st.out_begin, st.out_len = 0, (N if F else 0)
+            nch = max(1, len(b) - 1)
+            st.n_chunks = nch
+            st.chunk_first = b[1] if len(b) > 2 else 0
+            st.chunk_len = (b[2] - b[1]) if len(b) > 3 else max(1, (b[-1] - b[1]) if len(b) > 2 else 1)
+            st.in_scale, st.out_scale = 1.0, float(out_scale)
+            _set_gate(st, self.Ton, self.Toff)
+            streams.append(st)
+        self.y, out_offs = _alloc_out(torch, [s.out_len for s in streams], ss.ch, ss.x.device)
+        for st, o in zip(streams, out_offs):
+            st.out_off = o
+        desc = TomatisPlanDesc(n_fft=n_fft, hop=hop, ch=ss.ch, norm_mode=NORM_EPS,
+                               up_delay_frames=Dk, min_hold_frames=0, xfade_frames=xf,
+                               alpha_mode=1 if self.xfade else 0)
+        self.plan = Plan(desc, dsp.hann(n_fft), streams)
+        self.streams = list(self.plan.streams)[:len(streams)]
+        Ft = max(1, self.plan.total_frames)
+        dev = ss.x.device
+        self.r = torch.empty(Ft, dtype=torch.float32, device=dev)
+        self.states = torch.empty(Ft, dtype=torch.uint8, device=dev)
+        self.rows = torch.empty(Ft, dtype=torch.int16, device=dev)
+        self.alpha = torch.empty(Ft, dtype=torch.float64, device=dev) if self.xfade else None
+        self.peaks = torch.zeros(max(1, self.plan.total_chunks), dtype=torch.int32, device=dev)
+        self.gains = torch.from_numpy(np.stack(rows).astype(np.float32)).to(dev)
+        self.n_rows = len(rows)
+        self.out_offs = out_offs
+        self.g1_db, self.g2_db = g1_db, g2_db
+
+    def run(self):
+        L, P, hs = lib(), self.plan.h, stream_handle()
+        self.peaks.zero_()
+        check(L.tomatis_levels(P, ptr(self.ss.x), ptr(self.r), F32, hs), "levels")
+        check(L.tomatis_gate_std(P, ptr(self.r), ptr(self.states), ptr(self.rows),
+                                 ptr(self.alpha), hs), "gate_std")
+        check(L.tomatis_stft_ola(P, ptr(self.ss.x), ptr(self.gains), self.n_rows,
+                                 ptr(self.rows), ptr(self.y), ptr(self.peaks), hs), "stft_ola")
+        check(L.tomatis_apply_limiter(P, ptr(self.y), ptr(self.peaks), PEAK_LIMIT, hs),
+              "apply_limiter")
+        return self.result()
+
+    def result(self) -> Result:
+        st = self.streams
+        return Result(y=self.y, out_offs=self.out_offs, out_lens=[s.out_len for s in st],
+                      ch=self.ss.ch, frame_base=[s.frame_base for s in st],
+                      n_frames=[s.n_frames for s in st],
+                      first_start=[s.first_start for s in st], hop=self.hop,
+                      states=self.states, r=self.r, alpha=self.alpha,
+                      chunk_peaks=self.peaks, chunk_base=[s.chunk_base for s in st],
+                      n_chunks=[s.n_chunks for s in st],
+                      extra=dict(Ton=self.Ton, Toff=self.Toff, T=self.T, xfade_frames=self.xf,
+                                 up_delay_samples=self.up_delay_samples, bounds=self.bounds))
+
+
+def _alpha_lattice(xf: int):
+    """alpha values m*step reached by repeated +step from 0 (reference accumulation),
+    with the snapped end points 0.0 and 1.0 exact.  Rows 2+m of the gain table."""
+    if xf <= 0:
+        return [0.0, 1.0]
+    step = 1.0 / xf
+    out, a = [0.0], 0.0
+    for _ in range(1, xf):
+        a = a + step
+        out.append(a)
+    out.append(1.0)
+    return [np.float64(v) for v in out]
+
+
+# ---------------------------------------------------------------------------
+# adaptive
+# ---------------------------------------------------------------------------
+
+class AdaptivePipeline:
+    """process_tomatis_adaptive: attenuation, levels, bisection, min-hold gate,
+    alpha cross-fade, mixed gains, OLA, restore, global limiter."""
+
+    def __init__(self, ss: StreamSet, *, fc=1000.0, slope=12.0, c1_low=15.0, c1_high=-15.0,
+                 c2_low=-15.0, c2_high=15.0, target_c2=0.5, hyst_db=3.0, min_hold_ms=250.0,
+                 xfade_ms=500.0, headroom_margin=2.0, n_fft=4096, hop=2048):
+        torch = _torch()
+        _check_fft(n_fft, hop, ss.ch)
+        self.ss, self.n_fft, self.hop = ss, n_fft, hop
+        sr = ss.sr
+        frame_ms = hop / sr * 1000
+        self.mh = int(np.ceil(min_hold_ms / frame_ms))
+        self.xf = int(np.ceil(xfade_ms / frame_ms))
+        self.target_c2, self.hyst_db = target_c2, hyst_db
+        self.max_gain = max(abs(c1_low), abs(c2_high))
+        self.margin = headroom_margin
+        freqs = np.fft.rfftfreq(n_fft, 1 / sr)
+        c1_db = dsp.build_tilt_gain_db(freqs, fc, slope, c1_low, c1_high)
+        c2_db = dsp.build_tilt_gain_db(freqs, fc, slope, c2_low, c2_high)
+        xfe = self.xf if self.xf > 0 else 1
+        rows = [np.zeros(len(freqs), np.float32)] * 2  # rows 0/1 unused in adaptive mode
+        for a in _alpha_lattice(xfe):
+            rows.append((10 ** (np.asarray((1 - a) * c1_db + a * c2_db) / 20.0)).astype(np.float32))
+        streams = []
+        for off, N in zip(ss.offs, ss.lens):
+            k0, F, s0 = dsp.adaptive_frames(N, n_fft, hop)
+            st = TomatisStream()
+            st.in_off, st.n, st.first_start, st.n_frames = off, N, s0, F
+            st.out_begin, st.out_len = 0, (N if F else 0)
+            st.n_chunks, st.chunk_first, st.chunk_len = 1, 0, 1
+            st.in_scale, st.out_scale = 1.0, 1.0
+            streams.append(st)
+        self.y, out_offs = _alloc_out(torch, [s.out_len for s in streams], ss.ch, ss.x.device)
+        for st, o in zip(streams, out_offs):
+            st.out_off = o
+        desc = TomatisPlanDesc(n_fft=n_fft, hop=hop, ch=ss.ch, norm_mode=NORM_MAX,
+                               up_delay_frames=0, min_hold_frames=self.mh,
+                               xfade_frames=self.xf, alpha_mode=2)
+        self.plan = Plan(desc, dsp.hann(n_fft), streams)
+        Ft = max(1, self.plan.total_frames)
+        dev = ss.x.device
+        self.r32 = torch.empty(Ft, dtype=torch.float32, device=dev)
+        self.r64 = torch.empty(Ft, dtype=torch.float64, device=dev)
+        self.levels = torch.empty(Ft, dtype=torch.float64, device=dev)
+        self.states = torch.empty(Ft, dtype=torch.uint8, device=dev)
+        self.rows = torch.empty(Ft, dtype=torch.int16, device=dev)
+        self.alpha = torch.empty(Ft, dtype=torch.float64, device=dev)
+        self.t_out = torch.empty(max(1, ss.n_streams), dtype=torch.float64, device=dev)
+        self.peaks = torch.zeros(max(1, self.plan.total_chunks), dtype=torch.int32, device=dev)
+        self.inpk = torch.zeros(max(1, ss.n_streams), dtype=torch.int32, device=dev)
+        self.gains = torch.from_numpy(np.stack(rows)).to(dev)
+        self.n_rows = len(rows)
+        self.out_offs = out_offs
+
+    def run(self):
+        torch = _torch()
+        L, P, hs = lib(), self.plan.h, stream_handle()
+        ss = self.ss
+        sts = self.plan.streams
+        # 1. input peak per stream -> attenuation (process_tomatis_adaptive.py:201-215)
+        self.inpk.zero_()
+        for i in range(ss.n_streams):
+            n = ss.lens[i] * ss.ch
+            sub = ss.x[ss.offs[i]:ss.offs[i] + n]
+            check(L.tomatis_absmax(ptr(sub), n, ptr(self.inpk[i:i + 1]), hs), "absmax")
+        pk = self.inpk.cpu().numpy().astype(np.uint32).view(np.float32)
+        self.atten, prec = [], []
+        for i in range(ss.n_streams):
+            peak_db = 20 * np.log10(pk[i] + dsp.EPS)
+            atten_db = max(0, peak_db + self.max_gain + self.margin)
+            self.atten.append(atten_db)
+            if atten_db > 0:   # float32 pipeline (NEP 50)
+                sts[i].in_scale = float(10 ** (np.asarray(-atten_db) / 20.0))
+                sts[i].out_scale = float(10 ** (np.asarray(atten_db) / 20.0))
+                prec.append(F32)
+            else:              # float64 pipeline: x * 1.0
+                sts[i].in_scale, sts[i].out_scale = 1.0, 1.0
+                prec.append(F64)
+        self.plan.update()
+        # 2. per-frame levels (f32 and/or f64 r), host log10 exactly as numpy
+        if F32 in prec:
+            check(L.tomatis_levels(P, ptr(ss.x), ptr(self.r32), F32, hs), "levels f32")
+        if F64 in prec:
+            check(L.tomatis_levels(P, ptr(ss.x), ptr(self.r64), F64, hs), "levels f64")
+        r32 = self.r32.cpu().numpy() if F32 in prec else None
+        r64 = self.r64.cpu().numpy() if F64 in prec else None
+        lv = np.empty(self.plan.total_frames, np.float64)
+        tlh = np.empty((ss.n_streams, 3), np.float64)
+        for i in range(ss.n_streams):
+            a, F = sts[i].frame_base, sts[i].n_frames
+            r = (r32 if prec[i] == F32 else r64)[a:a + F]
+            lvi = dsp.r_to_level(r)
+            lv[a:a + F] = lvi
+            valid = lvi[lvi > -70]
+            if len(valid) == 0:
+                tlh[i] = (np.nan, np.nan, np.median(lvi) if F else 0.0)
+            else:
+                tlh[i] = (np.percentile(valid, 5), np.percentile(valid, 95), np.median(valid))
+        self.levels.copy_(torch.from_numpy(lv))
+        tl = torch.from_numpy(tlh.reshape(-1)).to(self.levels.device)
+        self._tlh = tl
+        # 3. bisection + min-hold states + alpha + rows
+        check(L.tomatis_minhold_bisect(P, ptr(self.levels), ptr(tl), self.target_c2,
+                                       self.hyst_db, ptr(self.t_out), ptr(self.states),
+                                       ptr(self.rows), ptr(self.alpha), hs), "minhold_bisect")
+        # 4. STFT-gain-OLA, normalise max(w,1e-8), restore, global limiter
+        self.peaks.zero_()
+        check(L.tomatis_stft_ola(P, ptr(ss.x), ptr(self.gains), self.n_rows, ptr(self.rows),
+                                 ptr(self.y), ptr(self.peaks), hs), "stft_ola")
+        check(L.tomatis_apply_limiter(P, ptr(self.y), ptr(self.peaks), PEAK_LIMIT, hs),
+              "apply_limiter")
+        self.prec = prec
+        return self.result()
+
+    def result(self) -> Result:
+        st = list(self.plan.streams)[:self.ss.n_streams]
+        return Result(y=self.y, out_offs=self.out_offs, out_lens=[s.out_len for s in st],
+                      ch=self.ss.ch, frame_base=[s.frame_base for s in st],
+                      n_frames=[s.n_frames for s in st],
+                      first_start=[s.first_start for s in st], hop=self.hop,
+                      states=self.states, r=self.r32, alpha=self.alpha,
+                      chunk_peaks=self.peaks, chunk_base=[s.chunk_base for s in st],
+                      n_chunks=[s.n_chunks for s in st],
+                      extra=dict(levels=self.levels, thresholds=self.t_out,
+                                 atten_db=getattr(self, "atten", None),
+                                 min_hold_frames=self.mh, xfade_frames=self.xf,
+                                 prec=getattr(self, "prec", None)))
+
+
+# ---------------------------------------------------------------------------
+# static EQ (layer2 / layer2b)
+# ---------------------------------------------------------------------------
+
+class StaticEqPipeline:
+    """One static gain row through the STFT-OLA (layer2_apply_eq with/without pad,
+    layer2b_apply_residual_eq = no pad).  Output keeps the head pad (layer2)."""
+
+    def __init__(self, ss: StreamSet, gain_bins: np.ndarray, *, n_fft=4096, hop=2048,
+                 pad=True, global_gain_db=0.0):
+        torch = _torch()
+        _check_fft(n_fft, hop, ss.ch)
+        self.ss, self.n_fft, self.hop = ss, n_fft, hop
+        pl = n_fft // 2 if pad else 0
+        g_global = 10.0 ** (global_gain_db / 20.0)
+        streams = []
+        for off, N in zip(ss.offs, ss.lens):
+            total = N + 2 * pl
+            F = (total - n_fft) // hop + 1 if total >= n_fft else 0
+            st = TomatisStream()
+            st.in_off, st.n, st.first_start, st.n_frames = off, N, -pl, F
+            st.out_begin = -pl
+            st.out_len = (F - 1) * hop + n_fft if F else 0
+            st.n_chunks, st.chunk_first, st.chunk_len = 1, 0, 1
+            st.in_scale, st.out_scale = float(np.float32(g_global)), 1.0
+            streams.append(st)
+        self.y, out_offs = _alloc_out(torch, [s.out_len for s in streams], ss.ch, ss.x.device)
+        for st, o in zip(streams, out_offs):
+            st.out_off = o
+        desc = TomatisPlanDesc(n_fft=n_fft, hop=hop, ch=ss.ch, norm_mode=NORM_EPS,
+                               up_delay_frames=0, min_hold_frames=0, xfade_frames=0,
+                               alpha_mode=0)
+        self.plan = Plan(desc, dsp.hann(n_fft), streams)
+        Ft = max(1, self.plan.total_frames)
+        dev = ss.x.device
+        self.rows = torch.zeros(Ft, dtype=torch.int16, device=dev)
+        self.peaks = torch.zeros(max(1, self.plan.total_chunks), dtype=torch.int32, device=dev)
+        self.gains = torch.from_numpy(np.asarray(gain_bins, np.float32)[None, :].copy()).to(dev)
+        self.out_offs = out_offs
+
+    def run(self):
+        L, P, hs = lib(), self.plan.h, stream_handle()
+        self.peaks.zero_()
+        check(L.tomatis_stft_ola(P, ptr(self.ss.x), ptr(self.gains), 1, ptr(self.rows),
+                                 ptr(self.y), ptr(self.peaks), hs), "stft_ola")
+        return self.result()
+
+    def result(self) -> Result:
+        st = list(self.plan.streams)[:self.ss.n_streams]
+        return Result(y=self.y, out_offs=self.out_offs, out_lens=[s.out_len for s in st],
+                      ch=self.ss.ch, frame_base=[s.frame_base for s in st],
+                      n_frames=[s.n_frames for s in st],
+                      first_start=[s.first_start for s in st], hop=self.hop,
+                      chunk_peaks=self.peaks, chunk_base=[s.chunk_base for s in st],
+                      n_chunks=[s.n_chunks for s in st])
+
+
+def scale_copy(src, scale: float):
+    """Device ``src * float32(scale)`` into a new tensor (layer-2 gain protect)."""
+    torch = _torch()
+    out = torch.empty_like(src)
+    check(lib().tomatis_scale_copy(ptr(src), ptr(out), src.numel(), float(np.float32(scale)),
+                                   stream_handle()), "scale_copy")
+    return out
+
+
+def frame_r(x: np.ndarray, sr: int, n_fft: int, hop: int, first_start: int, n_frames: int,
+            precision=F32, in_scale: float = 1.0) -> np.ndarray:
+    """Per-frame RMS r of one stream on the GPU (levels kernel), returned to host."""
+    torch = _torch()
+    ss = StreamSet.from_arrays([x], sr)
+    st = TomatisStream()
+    st.in_off, st.n, st.first_start, st.n_frames = 0, len(x), first_start, n_frames
+    st.out_begin, st.out_len, st.n_chunks, st.chunk_len = first_start, 0, 1, 1
+    st.in_scale, st.out_scale = in_scale, 1.0
+    desc = TomatisPlanDesc(n_fft=n_fft, hop=hop, ch=ss.ch, norm_mode=NORM_EPS,
+                           up_delay_frames=0, min_hold_frames=0, xfade_frames=0, alpha_mode=0)
+    plan = Plan(desc, dsp.hann(n_fft), [st])
+    dt = torch.float32 if precision == F32 else torch.float64
+    r = torch.empty(max(1, n_frames), dtype=dt, device=ss.x.device)
+    check(lib().tomatis_levels(plan.h, ptr(ss.x), ptr(r), precision, stream_handle()), "levels")
+    out = r[:n_frames].cpu().numpy()
+    plan.close()
+    return out
+
+
+def compute_frame_levels(x, sr, n_fft, hop, silence_threshold=-70):
+    """GPU version of process_tomatis_adaptive.compute_frame_levels
+    (src/process_tomatis_adaptive.py:57-84): (levels, valid_mask, times).
+
+    The input dtype decides the level precision as in the reference."""
+    x = np.asarray(x)
+    if x.ndim == 1:
+        x = x.reshape(-1, 1)
+    N = len(x)
+    k0, F, s0 = dsp.adaptive_frames(N, n_fft, hop)
+    prec = F64 if x.dtype == np.float64 else F32
+    if x.dtype == np.float64 and not np.array_equal(x.astype(np.float32).astype(np.float64), x):
+        raise ValueError("float64 input must be exactly representable in float32 "
+                         "(the reference feeds float32 PCM scaled by 1.0)")
+    r = frame_r(x.astype(np.float32), sr, n_fft, hop, s0, F, precision=prec)
+    levels = dsp.r_to_level(r)
+    valid = levels > silence_threshold
+    frame_sec = hop / sr
+    times = [(i + 1) * frame_sec for i in range(len(levels))]
+    return levels, valid, times
+
+
+def simulate_gate(levels, threshold_dbfs, hyst_db=3.0, min_hold_frames=6):
+    """GPU min-hold gate (src/process_tomatis_adaptive.py:87-121): list of 'C1'/'C2'."""
+    st = _minhold_states(np.asarray(levels, np.float64), [(np.nan, np.nan, threshold_dbfs)],
+                         hyst_db, min_hold_frames, 0.5)[0]
+    return ["C1" if s == 1 else "C2" for s in st]
+
+
+def find_optimal_threshold(levels, valid_mask, hyst_db=3.0, min_hold_frames=6, target_c2=0.5):
+    """GPU bisection (src/process_tomatis_adaptive.py:124-154)."""
+    levels = np.asarray(levels, np.float64)
+    valid = levels[valid_mask]
+    if len(valid) == 0:
+        return np.median(levels)
+    tlh = (np.percentile(valid, 5), np.percentile(valid, 95), np.median(valid))
+    return _minhold_states(levels, [tlh], hyst_db, min_hold_frames, target_c2)[1][0]
+
+
+def _minhold_states(levels, tlhs, hyst_db, mh, target):
+    torch = _torch()
+    F = len(levels)
+    st = TomatisStream()
+    st.n, st.first_start, st.n_frames = 0, 0, F
+    st.out_begin, st.out_len, st.n_chunks, st.chunk_len = 0, 0, 1, 1
+    st.in_scale, st.out_scale = 1.0, 1.0
+    desc = TomatisPlanDesc(n_fft=2048, hop=512, ch=1, norm_mode=NORM_MAX, up_delay_frames=0,
+                           min_hold_frames=mh, xfade_frames=1, alpha_mode=2)
+    plan = Plan(desc, dsp.hann(2048), [st])
+    dev = "cuda"
+    lv = torch.from_numpy(levels).to(dev)
+    tl = torch.tensor(np.asarray(tlhs, np.float64).reshape(-1), device=dev)
+    states = torch.empty(max(1, F), dtype=torch.uint8, device=dev)
+    t_out = torch.empty(1, dtype=torch.float64, device=dev)
+    check(lib().tomatis_minhold_bisect(plan.h, ptr(lv), ptr(tl), target, hyst_db, ptr(t_out),
+                                       ptr(states), None, None, stream_handle()), "minhold")
+    out = states[:F].cpu().numpy(), t_out.cpu().numpy()
+    plan.close()
+    return out
+
+
+__all__ = ["StreamSet", "Plan", "GatePipeline", "AdaptivePipeline", "StaticEqPipeline",
+           "Result", "scale_copy", "frame_r", "compute_frame_levels", "simulate_gate",
+           "find_optimal_threshold", "math"]
