@@ -1,0 +1,203 @@
+#!/usr/bin/env python3
+"""Benchmark: Msamples/s of the end-to-end STFT-gate-OLA hot path on MI355X.
+
+Default workload (BASELINE.json configs[1], "C2"): one 60-min stereo 44.1 kHz
+stream per GPU, standard mode (process_tomatis), n_fft=2048, hop=512, Hann,
+gate_ui=50 (log_percent, -40 dBFS), +-15 dB tilt.  A step = one pass of the
+whole device chain over the resident input: levels -> gate scan (3 kernels) ->
+fused STFT-gain-ISTFT-OLA-normalise -> limiter fix-up.  Input is seeded
+synthetic PCM generated on the device before timing.
+
+Contract: `python bench.py --gpus N --steps K --warmup W`; for N > 1 launched
+by torch.distributed.run (one rank per GPU, RCCL).  Multi-GPU = weak scaling:
+each rank owns its own stream(s); the only collective is an all_gather of the
+per-stream manifest records (after the timed region).  Rank 0 prints ONE JSON
+line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0         # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_PEAK_TFLOPS = 157.3      # MI355X vector FP32 (no packed-math doubling on gfx950)
+
+WORKLOADS = {
+    # name: (streams per GPU, seconds, sr, ch, mode, n_fft, hop, description)
+    "c2": (1, 3600, 44100, 2, "standard", 2048, 512,
+           "C2: 1 x 60 min stereo 44.1 kHz per GPU, standard mode, n_fft 2048 hop 512, "
+           "gate_ui 50 (log_percent)"),
+    "c4": (64, 300, 48000, 2, "standard", 2048, 512,
+           "C4: 64 x 5 min stereo 48 kHz per GPU (512 over 8 GPUs), standard, 2048/512"),
+    "c5x": (16, 300, 96000, 2, "xfade", 4096, 1024,
+            "C5 stage 1: 16 x 5 min stereo 96 kHz per GPU, xfade 500 ms, 4096/1024"),
+}
+
+
+def flops_per_ch_sample(n_fft: int, hop: int) -> float:
+    """per frame-channel 2*2.5*n*log2(n) + 2n + 2(n/2+1) + n."""
+    n = n_fft
+    per_frame_ch = 2 * 2.5 * n * np.log2(n) + 2 * n + 2 * (n // 2 + 1) + n
+    return per_frame_ch / hop
+
+
+def dist_init():
+    import torch
+    import torch.distributed as dist
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if ws > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group(backend="nccl", rank=rank, world_size=ws,
+                                device_id=torch.device("cuda", local))
+    return rank, ws, local
+
+
+def cpu_baseline(sample_s: int, sr: int, n_fft: int, hop: int, ch: int, x_host=None):
+    """Time the oracle ('port' of the reference loop) on one host core."""
+    from oracle import tomatis_oracle as orc
+    from tomatis_audio_processor_amd.synth import synth_stream
+    n = sample_s * sr
+    x = x_host if x_host is not None else synth_stream(1000, n, ch, sr)
+    t0 = time.perf_counter()
+    orc.process_standard(x, sr, gate_ui=50, n_fft=n_fft, hop=hop)
+    dt = time.perf_counter() - t0
+    return {"value": round(n * ch / dt / 1e6, 3), "unit": "Msamples/s", "cores": 1,
+            "kind": "port",
+            "sample": f"first {sample_s} s of stream seed 1000 ({n} x {ch} ch, {sr} Hz), "
+                      f"oracle/tomatis_oracle.process_standard (numpy {np.__version__}), "
+                      f"1 thread, {dt:.2f} s"}
+
+
+def load_traffic(workload: str):
+    """HBM bytes per launch of the fused kernel from the committed rocprofv3 PMC
+    summary (profiles/pmc_traffic.json), corrected as MI355X_MICROARCH.md
+    prescribes (FETCH_SIZE x 2 for wide streaming reads).  None if absent."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            return json.load(f).get(workload, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--cpu-sample-s", type=int, default=900,
+                    help="seconds of audio for the CPU baseline (0 disables)")
+    a = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    rank, ws, local = dist_init()
+    from tomatis_audio_processor_amd import engine
+
+    nstr, secs, sr, ch, mode, n_fft, hop, desc = WORKLOADS[a.workload]
+    n = secs * sr
+    ss = engine.StreamSet.synthetic(nstr, n, ch, sr, seed0=1000 + rank * nstr)
+    if mode == "standard":
+        pipe = engine.GatePipeline(ss, gate_ui=50, n_fft=n_fft, hop=hop)
+    else:
+        pipe = engine.GatePipeline(ss, gate_ui=50, gate_offset=-90, n_fft=n_fft, hop=hop,
+                                   xfade_ms=500.0)
+    torch.cuda.synchronize()
+
+    for _ in range(a.warmup):
+        pipe.run()
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    marks = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+             for _ in range(a.steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(a.steps):
+        pipe.run(marks=marks[k])
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in marks]))
+    if ws > 1:
+        tt = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(tt[0]), float(tt[1])
+
+    # per-stream manifest: (rank, stream, frames, C2 frames, max chunk peak bits)
+    res = pipe.result()
+    recs = []
+    for i in range(nstr):
+        st = res.states[res.frame_base[i]:res.frame_base[i] + res.n_frames[i]]
+        pk = res.chunk_peaks[res.chunk_base[i]:res.chunk_base[i] + res.n_chunks[i]].max()
+        recs.append(torch.stack([torch.tensor(rank, device="cuda"), torch.tensor(i, device="cuda"),
+                                 torch.tensor(res.n_frames[i], device="cuda"),
+                                 (st == 2).sum(), pk.to(torch.int64)]))
+    man = torch.stack(recs).to(torch.int64)
+    if ws > 1:
+        allm = [torch.empty_like(man) for _ in range(ws)]
+        dist.all_gather(allm, man)
+        man = torch.cat(allm)
+    man = man.cpu().numpy()
+
+    samples_per_step = n * ch * nstr * ws
+    value = samples_per_step * a.steps / elapsed / 1e6
+    ms_per_step = elapsed / a.steps * 1e3
+    # roofline of the dominant kernel (fused STFT-OLA), per launch on this rank
+    alg_bytes = 8.0 * n * ch * nstr
+    achieved_gbs = alg_bytes / (kern_ms * 1e-3) / 1e9
+    traffic = load_traffic(a.workload)
+    flops = flops_per_ch_sample(n_fft, hop) * n * ch * nstr
+    tflops = flops / (kern_ms * 1e-3) / 1e12
+
+    if rank == 0:
+        cpu = None
+        if a.cpu_sample_s > 0 and mode == "standard":
+            xs = ss.x[:a.cpu_sample_s * sr * ch].cpu().numpy().reshape(-1, ch)
+            cpu = cpu_baseline(a.cpu_sample_s, sr, n_fft, hop, ch, x_host=xs)
+        out = {
+            "metric": "Msamples/s (44.1 kHz stereo) end-to-end STFT-gate-OLA; % HBM roofline",
+            "value": round(value, 1), "unit": "Msamples/s", "n_gpus": ws, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (seeded device-generated noise, -20/-60 dBFS alternating 1.5 s)",
+            "config": {"workload": desc, "streams_per_gpu": nstr, "samples_per_channel": n,
+                       "channels": ch, "sr": sr, "mode": mode, "n_fft": n_fft, "hop": hop,
+                       "parallelism": f"file-parallel x{ws} (RCCL manifest all_gather)"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "k_stft_ola (fused frame/window/FFT/gain/IFFT/OLA/normalise)",
+                         "kernel_ms": round(kern_ms, 4),
+                         "alg_bytes_per_launch": alg_bytes},
+            "compute": {"bound": "valu-fp32", "achieved": round(tflops, 2),
+                        "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(tflops / FP32_PEAK_TFLOPS, 4),
+                        "flop_per_ch_sample": round(flops_per_ch_sample(n_fft, hop), 1)},
+            "cpu_baseline": cpu,
+            "manifest": {"streams": int(man.shape[0]),
+                         "c2_fraction": round(float(man[:, 3].sum() / max(1, man[:, 2].sum())), 4)},
+        }
+        print(json.dumps(out), flush=True)
+    if ws > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -119,11 +119,31 @@ __global__ __launch_bounds__(256) void k_levels(const float* __restrict__ x,
   const int span = (blk.nf - 1) * hop + n_fft;
   const T scale = (T)S.in_scale;
   const float* xs = x + S.in_off;
-  for (int i = threadIdx.x; i < span; i += blockDim.x) {
-    const int64_t p = span0 + i;
-    T v = (T)0;
-    if (p >= 0 && p < S.n) v = msq_of<T>(xs + p * ch, ch, scale);
-    lds[lidx<PAD>(i)] = v;
+  if (span0 >= 0 && span0 + span <= S.n && ch == 2) {
+    // interior: 8 independent 8-byte loads in flight per thread, then compute
+    const float2* src = reinterpret_cast<const float2*>(xs) + span0;
+    constexpr int U = 8;
+    for (int base = threadIdx.x; base < span; base += 256 * U) {
+      float2 t[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const int i = base + 256 * j;
+        t[j] = (i < span) ? src[i] : make_float2(0.f, 0.f);
+      }
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const int i = base + 256 * j;
+        const float pair[2] = {t[j].x, t[j].y};
+        if (i < span) lds[lidx<PAD>(i)] = msq_of<T>(pair, 2, scale);
+      }
+    }
+  } else {
+    for (int i = threadIdx.x; i < span; i += blockDim.x) {
+      const int64_t p = span0 + i;
+      T v = (T)0;
+      if (p >= 0 && p < S.n) v = msq_of<T>(xs + p * ch, ch, scale);
+      lds[lidx<PAD>(i)] = v;
+    }
   }
   __syncthreads();
   const int nleaf = n_fft >> 7;  // n_fft power of two >= 256
@@ -414,7 +434,7 @@ __global__ __launch_bounds__(1024) void k_minhold(const double* __restrict__ lev
 struct MainArgs {
   const float* x;
   float* y;
-  const float* gains;
+  const float* gains;   // [rows][N] gain per (lane, register) in bin layout (see gain_perm)
   const uint16_t* rows;
   uint32_t* peaks;
   const TomatisStream* st;
@@ -433,11 +453,11 @@ __device__ __forceinline__ float norm_den(float w, int mode) {
   return mode == TOMATIS_NORM_MAX ? fmaxf(w, 1e-8f) : (w + kEps32);
 }
 
-// wsum at position p, frames in ascending order (bit-exact with the reference's w_buf)
-__device__ float wsum_at(int64_t p, const TomatisStream& S, int hop, int N, const float* win2) {
-  const int64_t rel = p - S.first_start;
+// wsum at position rel = p - first_start, frames in ascending order (bit-exact
+// with the reference's w_buf)
+__device__ float wsum_rel(int64_t rel, int64_t n_frames, int hop, int N, const float* win2) {
   int64_t jhi = floordiv(rel, hop);
-  if (jhi > S.n_frames - 1) jhi = S.n_frames - 1;
+  if (jhi > n_frames - 1) jhi = n_frames - 1;
   int64_t jlo = floordiv(rel - N, hop) + 1;
   if (jlo < 0) jlo = 0;
   float w = 0.f;
@@ -455,15 +475,40 @@ template <int P>
 __device__ __forceinline__ void flush_peak(float& pk, int cid, const TomatisStream& S,
                                            uint32_t* peaks, int L) {
   const float m = wave_max(pk);  // P > 64: each wave flushes its partial max
-  if ((L & 63) == 0 && cid >= 0 && m > 0.f) atomicMax(peaks + S.chunk_base + cid, __float_as_uint(m));
+  if ((L & 63) == 0 && m > 0.f) atomicMax(peaks + S.chunk_base + cid, __float_as_uint(m));
   pk = 0.f;
 }
 
-template <int P, int SH, bool GENERIC>
+template <int CH>
+__device__ __forceinline__ cf load_cf(const float* xs, int64_t p) {
+  if constexpr (CH == 2) {
+    const float2 t = *reinterpret_cast<const float2*>(xs + 2 * p);
+    return {t.x, t.y};
+  } else {
+    return {xs[p], 0.f};
+  }
+}
+template <int CH>
+__device__ __forceinline__ void store_cf(float* ys, int64_t o, cf v) {
+  if constexpr (CH == 2) *reinterpret_cast<float2*>(ys + 2 * o) = make_float2(v.x, v.y);
+  else ys[o] = v.x;
+}
+template <int CH>
+__device__ __forceinline__ float cmag(cf v) {
+  if constexpr (CH == 2) return fmaxf(fabsf(v.x), fabsf(v.y));
+  else return fabsf(v.x);
+}
+
+// Fused framing -> window -> FFT -> gain -> IFFT -> window -> OLA -> normalise.
+// One sequence of P lanes processes frames [ka - (rmax-1), kb) of one stream
+// and emits the hop block of every frame >= ka.  Register OLA: lane L holds
+// positions s_k + L + P*i; the next frame's accumulator is the shift by SH.
+template <int P, int SH, int CH>
 __global__ __launch_bounds__(256) void k_stft_ola(MainArgs A) {
   using G = FftGeo<P>;
   constexpr int N = G::N;
   constexpr int NSEQ = 256 / P;
+  constexpr int HOP = SH * P;
   __shared__ cf s_twN[32 * P];
   __shared__ cf s_twP[P];
   __shared__ float s_win[N];
@@ -475,23 +520,20 @@ __global__ __launch_bounds__(256) void k_stft_ola(MainArgs A) {
 
   const int seq = threadIdx.x / P, L = threadIdx.x % P;
   const int run_id = blockIdx.x * NSEQ + seq;
-  // all sequences of the block iterate the same number of times when P > 64
   Run R{0, 0, 0, 0};
-  bool valid = run_id < A.n_runs;
+  const bool valid = run_id < A.n_runs;
   if (valid) R = A.runs[run_id];
   if constexpr (P <= 64) {
     if (!valid) return;
   }
   const TomatisStream S = A.st[R.s];
-  const int hop = A.hop;
   const int64_t kfirst = max<int64_t>(0, R.ka - (A.rmax - 1));
-  int64_t nit = valid ? (R.kb - kfirst) : 0;
+  int nit = valid ? (int)(R.kb - kfirst) : 0;
   if constexpr (P > 64) {
-    // block-uniform trip count
-    __shared__ int64_t s_nit[NSEQ];
+    __shared__ int s_nit[NSEQ];
     if (L == 0) s_nit[seq] = nit;
     __syncthreads();
-    int64_t m = 0;
+    int m = 0;
     for (int i = 0; i < NSEQ; ++i) m = max(m, s_nit[i]);
     nit = m;
   }
@@ -501,141 +543,195 @@ __global__ __launch_bounds__(256) void k_stft_ola(MainArgs A) {
   const int64_t out_end = S.out_begin + S.out_len;
   const float oscale = S.out_scale;
   const float iscale = S.in_scale;
+  const float* grows = A.gains;
 
-  // per-lane interior 1/wsum for the emitted offsets m = L + P*i, i < SH
-  float winv[GENERIC ? 1 : SH];
-  if constexpr (!GENERIC) {
+  float winv[SH];
 #pragma unroll
-    for (int i = 0; i < SH; ++i) winv[i] = A.winv[L + P * i];
-  }
-  // zeros before frame 0 (adaptive: first frame starts after the output start)
-  if (valid && R.ka == 0 && S.first_start > S.out_begin) {
-    for (int64_t p = S.out_begin + L; p < min(S.first_start, out_end); p += P) {
-      const int64_t o = (p - S.out_begin) * A.ch;
-      if (A.ch == 2) *reinterpret_cast<float2*>(ys + o) = make_float2(0.f, 0.f);
-      else ys[o] = 0.f;
-    }
+  for (int i = 0; i < SH; ++i) winv[i] = A.winv[L + P * i];
+
+  if (valid && R.ka == 0 && S.first_start > S.out_begin) {  // adaptive: zeros before frame 0
+    for (int64_t p = S.out_begin + L; p < min(S.first_start, out_end); p += P)
+      store_cf<CH>(ys, p - S.out_begin, cf{0.f, 0.f});
   }
 
-  cf acc[GENERIC ? 1 : (32 - SH)];
-  if constexpr (!GENERIC) {
-#pragma unroll
-    for (int i = 0; i < 32 - SH; ++i) acc[i] = {0.f, 0.f};
-  }
+  // chunk tracking by frame index (host guarantees hop-aligned chunk boundaries)
+  const int64_t s_ka = S.first_start + R.ka * HOP;
+  int cid = chunk_of(s_ka, S);
+  int64_t next_chunk_k = INT64_MAX;
+  if (S.n_chunks > 1 && cid < S.n_chunks - 1)
+    next_chunk_k = (S.chunk_first + (int64_t)cid * S.chunk_len - S.first_start) / HOP;
+  const int64_t chunk_k_step = S.n_chunks > 1 ? S.chunk_len / HOP : 0;
   float pk = 0.f;
-  int cid = -1;
 
-  for (int64_t it = 0; it < nit; ++it) {
+  cf acc[32 - SH];
+#pragma unroll
+  for (int i = 0; i < 32 - SH; ++i) acc[i] = {0.f, 0.f};
+
+  for (int it = 0; it < nit; ++it) {
     const int64_t k = kfirst + it;
     const bool live = valid && (k < R.kb);
-    const int64_t s_k = S.first_start + k * hop;
+    const int64_t s_k = S.first_start + k * HOP;
     cf v[32];
     // ---- load + analysis window ----
     const bool interior = (s_k >= 0) && (s_k + N <= S.n);
+    if (live && interior) {
+      const float* xf = xs + CH * s_k;
 #pragma unroll
-    for (int n2 = 0; n2 < 32; ++n2) {
-      const int64_t p = s_k + L + P * n2;
-      cf z = {0.f, 0.f};
-      if (live && (interior || (p >= 0 && p < S.n))) {
-        if (A.ch == 2) {
-          const float2 t = *reinterpret_cast<const float2*>(xs + 2 * p);
-          z = {t.x * iscale, t.y * iscale};
-        } else {
-          z = {xs[p] * iscale, 0.f};
-        }
-      }
-      const float w = s_win[L + P * n2];
-      v[n2] = {z.x * w, z.y * w};
-    }
-    fft_fwd<P>(v, L, s_twN, s_twP, buf);
-    // ---- gain row (real, even) and 1/N ----
-    {
-      const uint16_t row = live ? A.rows[S.frame_base + k] : 0;
-      const float* g = A.gains + (int64_t)row * A.n_bins;
+      for (int n2 = 0; n2 < 32; ++n2) v[n2] = load_cf<CH>(xf, L + P * n2);
+    } else {
 #pragma unroll
-      for (int i = 0; i < 32; ++i) {
-        int b = fft_bin<P>(L, i);
-        b = (b <= N / 2) ? b : N - b;
-        const float gg = g[b] * A.inv_n;
-        v[i] = cscale(v[i], gg);
+      for (int n2 = 0; n2 < 32; ++n2) {
+        const int64_t p = s_k + L + P * n2;
+        v[n2] = (live && p >= 0 && p < S.n) ? load_cf<CH>(xs, p) : cf{0.f, 0.f};
       }
     }
-    fft_inv<P>(v, L, s_twN, s_twP, buf);
-    // ---- synthesis window ----
+    const uint16_t row = live ? A.rows[S.frame_base + k] : 0;
+    if (iscale != 1.0f) {  // (x * scale) * win, two roundings as the reference
+#pragma unroll
+      for (int n2 = 0; n2 < 32; ++n2) v[n2] = cscale(v[n2], iscale);
+    }
 #pragma unroll
     for (int n2 = 0; n2 < 32; ++n2) v[n2] = cscale(v[n2], s_win[L + P * n2]);
-
-    if constexpr (GENERIC) {
-      if (live) {
-        cf* dst = A.scratch + (S.frame_base + k) * (int64_t)N;
+    fft_fwd<P>(v, L, s_twN, s_twP, buf);
+    // ---- gain row (real, even, 1/N folded in), coalesced per-lane layout ----
+    {
+      const float* g = grows + (int64_t)row * N;
 #pragma unroll
-        for (int n2 = 0; n2 < 32; ++n2) dst[L + P * n2] = v[n2];
+      for (int i = 0; i < 32; ++i) v[i] = cscale(v[i], g[i * P + L]);
+    }
+    fft_inv<P>(v, L, s_twN, s_twP, buf);
+    // ---- synthesis window + register OLA ----
+#pragma unroll
+    for (int n2 = 0; n2 < 32; ++n2) v[n2] = cscale(v[n2], s_win[L + P * n2]);
+#pragma unroll
+    for (int i = 0; i < 32 - SH; ++i) v[i] = v[i] + acc[i];
+    if (live && k >= R.ka) {
+      if (k == next_chunk_k) {
+        flush_peak<P>(pk, cid, S, A.peaks, L);
+        ++cid;
+        next_chunk_k = (cid < S.n_chunks - 1) ? next_chunk_k + chunk_k_step : INT64_MAX;
       }
-    } else {
-      // ---- register OLA: v[n2] += acc[n2] (positions s_k + L + P*n2) ----
-#pragma unroll
-      for (int i = 0; i < 32 - SH; ++i) v[i] = v[i] + acc[i];
-      const bool emit = live && (k >= R.ka);
+      const bool full = (s_k >= S.out_begin) && (s_k + HOP <= out_end);
       const bool edge = (k < A.rmax - 1);
-      if (emit) {
-        const int c0 = chunk_of(s_k, S), c1 = chunk_of(s_k + hop - 1, S);
-        if (c0 != cid) {
-          flush_peak<P>(pk, cid, S, A.peaks, L);
-          cid = c0;
+      if (full && !edge) {
+        float* yb = ys + CH * (s_k - S.out_begin);
+#pragma unroll
+        for (int i = 0; i < SH; ++i) {
+          const cf o = cscale(cscale(v[i], winv[i]), oscale);
+          store_cf<CH>(yb, L + P * i, o);
+          pk = fmaxf(pk, cmag<CH>(o));
         }
-        float pk1 = 0.f;
+      } else {
 #pragma unroll
         for (int i = 0; i < SH; ++i) {
           const int64_t p = s_k + L + P * i;
           if (p >= S.out_begin && p < out_end) {
-            cf o;
-            if (!edge) {
-              o = cscale(v[i], winv[i]);
-            } else {
-              const float d = norm_den(wsum_at(p, S, hop, N, A.win2), A.norm_mode);
-              o = {v[i].x / d, v[i].y / d};
-            }
-            o = cscale(o, oscale);
-            const int64_t oi = (p - S.out_begin) * A.ch;
-            if (A.ch == 2) *reinterpret_cast<float2*>(ys + oi) = make_float2(o.x, o.y);
-            else ys[oi] = o.x;
-            const float mag = (A.ch == 2) ? fmaxf(fabsf(o.x), fabsf(o.y)) : fabsf(o.x);
-            if (c0 == c1 || chunk_of(p, S) == c0) pk = fmaxf(pk, mag);
-            else pk1 = fmaxf(pk1, mag);
-          }
-        }
-        if (c1 != c0) {
-          flush_peak<P>(pk, cid, S, A.peaks, L);
-          cid = c1;
-          pk = pk1;
-        }
-        // tail of the stream: positions after the last frame's first hop
-        if (R.last && k == R.kb - 1) {
-#pragma unroll
-          for (int i = SH; i < 32; ++i) {
-            const int64_t p = s_k + L + P * i;
-            if (p >= S.out_begin && p < out_end) {
-              const float d = norm_den(wsum_at(p, S, hop, N, A.win2), A.norm_mode);
-              cf o = {v[i].x / d, v[i].y / d};
-              o = cscale(o, oscale);
-              const int64_t oi = (p - S.out_begin) * A.ch;
-              if (A.ch == 2) *reinterpret_cast<float2*>(ys + oi) = make_float2(o.x, o.y);
-              else ys[oi] = o.x;
-              const float mag = (A.ch == 2) ? fmaxf(fabsf(o.x), fabsf(o.y)) : fabsf(o.x);
-              const int c = chunk_of(p, S);
-              if (c == cid) pk = fmaxf(pk, mag);
-            }
+            const float d = norm_den(wsum_rel(p - S.first_start, S.n_frames, HOP, N, A.win2),
+                                     A.norm_mode);
+            const cf o = cscale(cf{v[i].x / d, v[i].y / d}, oscale);
+            store_cf<CH>(ys, p - S.out_begin, o);
+            pk = fmaxf(pk, cmag<CH>(o));
           }
         }
       }
-      // ---- shift the accumulator by one hop ----
+      if (R.last && k == R.kb - 1) {  // stream tail after the last frame
 #pragma unroll
-      for (int i = 0; i < 32 - SH; ++i) acc[i] = v[i + SH];
+        for (int i = SH; i < 32; ++i) {
+          const int64_t p = s_k + L + P * i;
+          if (p >= S.out_begin && p < out_end) {
+            const float d = norm_den(wsum_rel(p - S.first_start, S.n_frames, HOP, N, A.win2),
+                                     A.norm_mode);
+            const cf o = cscale(cf{v[i].x / d, v[i].y / d}, oscale);
+            store_cf<CH>(ys, p - S.out_begin, o);
+            pk = fmaxf(pk, cmag<CH>(o));
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 32 - SH; ++i) acc[i] = v[i + SH];
+  }
+  if (valid) flush_peak<P>(pk, cid, S, A.peaks, L);
+}
+
+// Generic hop: same transform, windowed frame outputs to scratch, then a gather.
+template <int P>
+__global__ __launch_bounds__(256) void k_stft_frames(MainArgs A) {
+  using G = FftGeo<P>;
+  constexpr int N = G::N;
+  constexpr int NSEQ = 256 / P;
+  __shared__ cf s_twN[32 * P];
+  __shared__ cf s_twP[P];
+  __shared__ float s_win[N];
+  __shared__ cf s_buf[NSEQ][G::BUF];
+  for (int i = threadIdx.x; i < 32 * P; i += 256) s_twN[i] = A.twN[i];
+  for (int i = threadIdx.x; i < P; i += 256) s_twP[i] = A.twP[i];
+  for (int i = threadIdx.x; i < N; i += 256) s_win[i] = A.win[i];
+  __syncthreads();
+  const int seq = threadIdx.x / P, L = threadIdx.x % P;
+  const int run_id = blockIdx.x * NSEQ + seq;
+  Run R{0, 0, 0, 0};
+  const bool valid = run_id < A.n_runs;
+  if (valid) R = A.runs[run_id];
+  if constexpr (P <= 64) {
+    if (!valid) return;
+  }
+  const TomatisStream S = A.st[R.s];
+  int nit = valid ? (int)(R.kb - R.ka) : 0;
+  if constexpr (P > 64) {
+    __shared__ int s_nit[NSEQ];
+    if (L == 0) s_nit[seq] = nit;
+    __syncthreads();
+    int m = 0;
+    for (int i = 0; i < NSEQ; ++i) m = max(m, s_nit[i]);
+    nit = m;
+  }
+  cf* buf = s_buf[seq];
+  const float* xs = A.x + S.in_off;
+  const int hop = A.hop;
+  for (int it = 0; it < nit; ++it) {
+    const int64_t k = R.ka + it;
+    const bool live = valid && (k < R.kb);
+    const int64_t s_k = S.first_start + k * hop;
+    cf v[32];
+#pragma unroll
+    for (int n2 = 0; n2 < 32; ++n2) {
+      const int64_t p = s_k + L + P * n2;
+      cf z = {0.f, 0.f};
+      if (live && p >= 0 && p < S.n) {
+        if (A.ch == 2) z = load_cf<2>(xs, p);
+        else z = load_cf<1>(xs, p);
+      }
+      const float w = s_win[L + P * n2];
+      v[n2] = {(z.x * S.in_scale) * w, (z.y * S.in_scale) * w};
+    }
+    fft_fwd<P>(v, L, s_twN, s_twP, buf);
+    const uint16_t row = live ? A.rows[S.frame_base + k] : 0;
+    const float* g = A.gains + (int64_t)row * N;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) v[i] = cscale(v[i], g[i * P + L]);
+    fft_inv<P>(v, L, s_twN, s_twP, buf);
+    if (live) {
+      cf* dst = A.scratch + (S.frame_base + k) * (int64_t)N;
+#pragma unroll
+      for (int n2 = 0; n2 < 32; ++n2) dst[L + P * n2] = cscale(v[n2], s_win[L + P * n2]);
     }
   }
-  if constexpr (!GENERIC) {
-    if (valid) flush_peak<P>(pk, cid, S, A.peaks, L);
-  }
+}
+
+// gain rows [rows][n_bins] -> [rows][N] in the per-lane bin layout of fft_fwd,
+// mirrored (real even gain) and scaled by 1/N (exact: power of two)
+template <int P>
+__global__ void k_gain_perm(const float* __restrict__ g, int n_rows, int n_bins,
+                            float* __restrict__ out) {
+  constexpr int N = 32 * P;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_rows * N) return;
+  const int row = t / N, e = t - row * N;
+  const int i = e / P, L = e - i * P;
+  int b = fft_bin<P>(L, i);
+  b = (b <= N / 2) ? b : N - b;
+  out[t] = g[(int64_t)row * n_bins + b] * (1.0f / (float)N);
 }
 
 // generic-hop OLA gather: one thread per output position (frame order preserved)
@@ -800,6 +896,8 @@ struct tomatis_plan_s {
   uint16_t* mh_tf = nullptr;
   int32_t* mh_cnt = nullptr;
   int64_t* mh_off = nullptr;
+  float* gperm = nullptr;
+  int gperm_rows = 0;
 };
 
 namespace {
@@ -828,9 +926,10 @@ int env_int(const char* name, int dflt) {
 
 int launch_check() { return hipfail(hipGetLastError()); }
 
-template <int P, int SH, bool GEN>
-void launch_main(const MainArgs& A, int nseq_blocks, hipStream_t s) {
-  hipLaunchKernelGGL((k_stft_ola<P, SH, GEN>), dim3(nseq_blocks), dim3(256), 0, s, A);
+template <int P, int SH>
+void launch_main(const MainArgs& A, int ch, int nseq_blocks, hipStream_t s) {
+  if (ch == 2) hipLaunchKernelGGL((k_stft_ola<P, SH, 2>), dim3(nseq_blocks), dim3(256), 0, s, A);
+  else hipLaunchKernelGGL((k_stft_ola<P, SH, 1>), dim3(nseq_blocks), dim3(256), 0, s, A);
 }
 
 }  // namespace
@@ -854,7 +953,7 @@ int tomatis_plan_destroy(tomatis_plan_t p) {
   if (!p) return TOMATIS_OK;
   void* ptrs[] = {p->st, p->runs, p->lblocks, p->segs, p->seg_first, p->seg_count, p->tf,
                   p->seg_start, p->win, p->win2, p->winv, p->twN, p->twP, p->scratch,
-                  p->pos_base, p->chunks, p->mh_tf, p->mh_cnt, p->mh_off};
+                  p->pos_base, p->chunks, p->mh_tf, p->mh_cnt, p->mh_off, p->gperm};
   for (void* q : ptrs) dfree(q);
   delete p;
   return TOMATIS_OK;
@@ -1042,6 +1141,11 @@ int tomatis_plan_create(tomatis_plan_t* out, const TomatisPlanDesc* desc, const 
   p->P = N / 32;
   p->SH = (hop % p->P == 0) ? hop / p->P : 0;
   p->generic = !(p->SH == 4 || p->SH == 8 || p->SH == 16);
+  for (int i = 0; i < n_streams && !p->generic; ++i) {
+    const TomatisStream& s = streams[i];
+    if (s.n_chunks > 1 && (((s.chunk_first - s.first_start) % hop) != 0 || (s.chunk_len % hop) != 0))
+      p->generic = true;  // chunk boundaries not on emit blocks: per-sample gather path
+  }
   int64_t fb = 0;
   int32_t cb = 0;
   for (int i = 0; i < n_streams; ++i) {
@@ -1165,10 +1269,23 @@ int tomatis_stft_ola(tomatis_plan_t p, const float* x, const float* gains, int32
   if (!p || !x || !gains || !rows || !y || !peaks || n_rows < 1) return TOMATIS_E_ARG;
   if (p->n_runs == 0) return TOMATIS_OK;
   hipStream_t s = (hipStream_t)hs;
+  const int N = p->d.n_fft;
+  if (n_rows > p->gperm_rows) {  // grows only; reuse across calls (graph-safe after first call)
+    dfree(p->gperm);
+    p->gperm = nullptr;
+    if (hipMalloc(reinterpret_cast<void**>(&p->gperm), (size_t)n_rows * N * sizeof(float)))
+      return TOMATIS_E_NOMEM;
+    p->gperm_rows = n_rows;
+  }
+  const int nb = (n_rows * N + 255) / 256;
+  if (p->P == 64)
+    hipLaunchKernelGGL(k_gain_perm<64>, dim3(nb), dim3(256), 0, s, gains, n_rows, N / 2 + 1, p->gperm);
+  else
+    hipLaunchKernelGGL(k_gain_perm<128>, dim3(nb), dim3(256), 0, s, gains, n_rows, N / 2 + 1, p->gperm);
   MainArgs A;
   A.x = x;
   A.y = y;
-  A.gains = gains;
+  A.gains = p->gperm;
   A.rows = rows;
   A.peaks = peaks;
   A.st = p->st;
@@ -1181,29 +1298,33 @@ int tomatis_stft_ola(tomatis_plan_t p, const float* x, const float* gains, int32
   A.scratch = p->scratch;
   A.n_runs = p->n_runs;
   A.hop = p->d.hop;
-  A.n_bins = p->d.n_fft / 2 + 1;
+  A.n_bins = N / 2 + 1;
   A.ch = p->d.ch;
   A.norm_mode = p->d.norm_mode;
   A.rmax = p->generic ? 1 : p->rmax;
-  A.inv_n = 1.0f / (float)p->d.n_fft;
+  A.inv_n = 1.0f / (float)N;
   const int nseq = 256 / p->P;
   const int blocks = (p->n_runs + nseq - 1) / nseq;
-  if (p->P == 64) {
-    if (p->generic) launch_main<64, 1, true>(A, blocks, s);
-    else if (p->SH == 4) launch_main<64, 4, false>(A, blocks, s);
-    else if (p->SH == 8) launch_main<64, 8, false>(A, blocks, s);
-    else launch_main<64, 16, false>(A, blocks, s);
-  } else {
-    if (p->generic) launch_main<128, 1, true>(A, blocks, s);
-    else if (p->SH == 4) launch_main<128, 4, false>(A, blocks, s);
-    else if (p->SH == 8) launch_main<128, 8, false>(A, blocks, s);
-    else launch_main<128, 16, false>(A, blocks, s);
+  const int ch = p->d.ch;
+  if (p->generic) {
+    if (p->P == 64) hipLaunchKernelGGL(k_stft_frames<64>, dim3(blocks), dim3(256), 0, s, A);
+    else hipLaunchKernelGGL(k_stft_frames<128>, dim3(blocks), dim3(256), 0, s, A);
+    int rc = launch_check();
+    if (rc || p->total_out == 0) return rc;
+    const int64_t ng = (p->total_out + 255) / 256;
+    hipLaunchKernelGGL(k_ola_gather, dim3((unsigned)ng), dim3(256), 0, s, A, p->n_streams,
+                       p->pos_base, p->total_out, N);
+    return launch_check();
   }
-  int rc = launch_check();
-  if (rc || !p->generic || p->total_out == 0) return rc;
-  const int64_t nb = (p->total_out + 255) / 256;
-  hipLaunchKernelGGL(k_ola_gather, dim3((unsigned)nb), dim3(256), 0, s, A, p->n_streams,
-                     p->pos_base, p->total_out, p->d.n_fft);
+  if (p->P == 64) {
+    if (p->SH == 4) launch_main<64, 4>(A, ch, blocks, s);
+    else if (p->SH == 8) launch_main<64, 8>(A, ch, blocks, s);
+    else launch_main<64, 16>(A, ch, blocks, s);
+  } else {
+    if (p->SH == 4) launch_main<128, 4>(A, ch, blocks, s);
+    else if (p->SH == 8) launch_main<128, 8>(A, ch, blocks, s);
+    else launch_main<128, 16>(A, ch, blocks, s);
+  }
   return launch_check();
 }
 

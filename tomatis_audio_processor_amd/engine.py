@@ -262,14 +262,22 @@ class GatePipeline:
         self.out_offs = out_offs
         self.g1_db, self.g2_db = g1_db, g2_db
 
-    def run(self):
+    def run(self, marks=None):
+        """Launch the whole chain on the current stream (no host sync).
+
+        ``marks``: optional pair of torch.cuda.Event recorded on this stream
+        around the fused STFT-OLA launch (bench.py's live kernel timing)."""
         L, P, hs = lib(), self.plan.h, stream_handle()
         self.peaks.zero_()
         check(L.tomatis_levels(P, ptr(self.ss.x), ptr(self.r), F32, hs), "levels")
         check(L.tomatis_gate_std(P, ptr(self.r), ptr(self.states), ptr(self.rows),
                                  ptr(self.alpha), hs), "gate_std")
+        if marks:
+            marks[0].record()
         check(L.tomatis_stft_ola(P, ptr(self.ss.x), ptr(self.gains), self.n_rows,
                                  ptr(self.rows), ptr(self.y), ptr(self.peaks), hs), "stft_ola")
+        if marks:
+            marks[1].record()
         check(L.tomatis_apply_limiter(P, ptr(self.y), ptr(self.peaks), PEAK_LIMIT, hs),
               "apply_limiter")
         return self.result()
