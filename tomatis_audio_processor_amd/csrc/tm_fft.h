@@ -19,17 +19,17 @@
 
 namespace tdsp {
 
-template <int P_>
+template <int P_, int NR_ = 32>
 struct FftGeo {
   static constexpr int P = P_;
-  static constexpr int NR = 32;             // complex registers per lane
+  static constexpr int NR = NR_;            // complex registers per lane
   static constexpr int N = NR * P;          // transform size
   static constexpr int PB = P / 8;          // step-3a size
   static constexpr int NJ = NR / PB;        // step-3a transforms per lane
   static constexpr int RW = P + 8;          // LDS row stride (complex)
   static constexpr int ROUNDS = NR / PB;    // exchange rounds
   static constexpr int BUF = PB * RW;       // complex per round buffer
-  static_assert(PB >= 4 && PB <= 32, "P in [32, 256]");
+  static_assert(PB >= 4 && PB <= NR && NR % 8 == 0, "need 4 <= P/8 <= NR, NR % 8 == 0");
 };
 
 // LDS synchronisation for an exchange: wave-local when P == 64.
@@ -49,17 +49,17 @@ __device__ __forceinline__ int x2col(int a, int c) { return 8 * c + (a ^ (c & 7)
 
 // forward FFT.  v: 32 registers (input x[L + P*n2]); out: bin layout above.
 // twN: LDS [32][P] with W_N^{n1*k2}; twP: LDS [P] with W_P^m; buf: round buffer.
-template <int P>
-__device__ __forceinline__ void fft_fwd(cf (&v)[32], int L, const cf* twN, const cf* twP,
+template <int P, int NR = 32>
+__device__ __forceinline__ void fft_fwd(cf (&v)[NR], int L, const cf* twN, const cf* twP,
                                         cf* buf) {
-  using G = FftGeo<P>;
+  using G = FftGeo<P, NR>;
   constexpr int PB = G::PB, RW = G::RW;
   const int a1 = L & 7, q1 = L >> 3;
   const int c3 = L % PB, q3 = L / PB;
   // step 1
-  dft<32, false, 0, 1, 32>(v);
+  dft<NR, false, 0, 1, NR>(v);
   // step 2
-  sfor<1, 32>([&](auto kk) {
+  sfor<1, NR>([&](auto kk) {
     constexpr int K = decltype(kk)::value;
     v[K] = cmul(v[K], twN[K * P + L]);
   });
@@ -80,7 +80,7 @@ __device__ __forceinline__ void fft_fwd(cf (&v)[32], int L, const cf* twN, const
   // step 3a: DFT_PB over b for each j
   sfor<0, G::NJ>([&](auto jj) {
     constexpr int J = decltype(jj)::value;
-    dft<PB, false, J * PB, 1, 32>(v);
+    dft<PB, false, J * PB, 1, NR>(v);
   });
   // step 3b: W_P^{a c}
   sfor<1, PB>([&](auto cc) {
@@ -110,30 +110,30 @@ __device__ __forceinline__ void fft_fwd(cf (&v)[32], int L, const cf* twN, const
     xsync<P>();
   });
   // step 3c: DFT_8 over a
-  sfor<0, 4>([&](auto jj) {
+  sfor<0, NR / 8>([&](auto jj) {
     constexpr int J = decltype(jj)::value;
-    dft<8, false, J * 8, 1, 32>(v);
+    dft<8, false, J * 8, 1, NR>(v);
   });
 }
 
 // inverse (unnormalised) FFT: bin layout -> v[n2] = x[L + P*n2] * N
-template <int P>
-__device__ __forceinline__ void fft_inv(cf (&v)[32], int L, const cf* twN, const cf* twP,
+template <int P, int NR = 32>
+__device__ __forceinline__ void fft_inv(cf (&v)[NR], int L, const cf* twN, const cf* twP,
                                         cf* buf) {
-  using G = FftGeo<P>;
+  using G = FftGeo<P, NR>;
   constexpr int PB = G::PB, RW = G::RW;
   const int a1 = L & 7, q1 = L >> 3;
   const int c3 = L % PB, q3 = L / PB;
   // step 3c': IDFT_8 over d -> a
-  sfor<0, 4>([&](auto jj) {
+  sfor<0, NR / 8>([&](auto jj) {
     constexpr int J = decltype(jj)::value;
-    dft<8, true, J * 8, 1, 32>(v);
+    dft<8, true, J * 8, 1, NR>(v);
   });
   // step 3b': conj W_P^{a c3}
   sfor<1, 8>([&](auto aa) {
     constexpr int A = decltype(aa)::value;
     const cf w = twP[(A * c3) & (P - 1)];
-    sfor<0, 4>([&](auto jj) {
+    sfor<0, NR / 8>([&](auto jj) {
       constexpr int J = decltype(jj)::value;
       v[J * 8 + A] = cmulc(v[J * 8 + A], w);
     });
@@ -159,7 +159,7 @@ __device__ __forceinline__ void fft_inv(cf (&v)[32], int L, const cf* twN, const
   // step 3a': IDFT_PB over c -> b
   sfor<0, G::NJ>([&](auto jj) {
     constexpr int J = decltype(jj)::value;
-    dft<PB, true, J * PB, 1, 32>(v);
+    dft<PB, true, J * PB, 1, NR>(v);
   });
   // exchange 4 : (lane (a,q), reg (j,b)) -> (lane n1, reg k2)
   sfor<0, G::ROUNDS>([&](auto rr) {
@@ -176,21 +176,21 @@ __device__ __forceinline__ void fft_inv(cf (&v)[32], int L, const cf* twN, const
     xsync<P>();
   });
   // step 2': conj W_N^{n1 k2}
-  sfor<1, 32>([&](auto kk) {
+  sfor<1, NR>([&](auto kk) {
     constexpr int K = decltype(kk)::value;
     v[K] = cmulc(v[K], twN[K * P + L]);
   });
-  // step 1': IDFT_32 over k2 -> n2
-  dft<32, true, 0, 1, 32>(v);
+  // step 1': IDFT_NR over k2 -> n2
+  dft<NR, true, 0, 1, NR>(v);
 }
 
 // bin index held by lane L, register index i (= j'*8 + d) after fft_fwd
-template <int P>
+template <int P, int NR = 32>
 __device__ __forceinline__ int fft_bin(int L, int i) {
   constexpr int PB = P / 8;
   const int c3 = L % PB, q3 = L / PB;
   const int jp = i >> 3, d = i & 7;
-  return (q3 + 8 * jp) + 32 * (c3 + PB * d);
+  return (q3 + 8 * jp) + NR * (c3 + PB * d);
 }
 
 }  // namespace tdsp

@@ -445,7 +445,7 @@ struct MainArgs {
   const cf* twP;        // [P]
   const float* winv;    // [hop] 1/(interior wsum) (already normalisation-rule applied)
   cf* scratch;          // generic path: [frames][N]
-  int n_runs, hop, n_bins, ch, norm_mode, rmax;
+  int n_runs, hop, n_bins, ch, norm_mode, rmax, n_rows_lds;
   float inv_n;
 };
 
@@ -499,27 +499,63 @@ __device__ __forceinline__ float cmag(cf v) {
   else return fabsf(v.x);
 }
 
+// ---- buffer-resource memory ops: one 32-bit lane offset + SGPR/immediate offsets
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mk_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+template <int CH>
+__device__ __forceinline__ cf bload(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  if constexpr (CH == 2) {
+    const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
+    return {__uint_as_float(t.x), __uint_as_float(t.y)};
+  } else {
+    return {__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0)), 0.f};
+  }
+}
+template <int CH>
+__device__ __forceinline__ void bstore(cf v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  if constexpr (CH == 2) {
+    const u32x2 t = {__float_as_uint(v.x), __float_as_uint(v.y)};
+    __builtin_amdgcn_raw_buffer_store_b64(t, r, voff, soff, 0);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.x), r, voff, soff, 0);
+  }
+}
+__device__ __forceinline__ float bloadf(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+
 // Fused framing -> window -> FFT -> gain -> IFFT -> window -> OLA -> normalise.
-// One sequence of P lanes processes frames [ka - (rmax-1), kb) of one stream
-// and emits the hop block of every frame >= ka.  Register OLA: lane L holds
-// positions s_k + L + P*i; the next frame's accumulator is the shift by SH.
-template <int P, int SH, int CH>
-__global__ __launch_bounds__(256) void k_stft_ola(MainArgs A) {
-  using G = FftGeo<P>;
+// One sequence of P lanes (P/64 waves) processes frames [ka - (rmax-1), kb) of
+// one stream and emits the hop block of every frame >= ka.  Lane L register i
+// holds stream position s_k + L + P*i; the OLA accumulator for the next frame
+// is this frame's registers shifted by SH = hop/P.
+// GLDS: the (<= 2) gain rows live in LDS in the per-lane layout.
+template <int P, int NR, int SH, int CH, bool GLDS>
+__global__ __launch_bounds__(256, 2) void k_stft_ola(MainArgs A) {
+  using G = FftGeo<P, NR>;
   constexpr int N = G::N;
   constexpr int NSEQ = 256 / P;
   constexpr int HOP = SH * P;
-  __shared__ cf s_twN[32 * P];
+  constexpr int NC = NR - SH;  // carried accumulator registers
+  __shared__ cf s_twN[NR * P];
   __shared__ cf s_twP[P];
   __shared__ float s_win[N];
   __shared__ cf s_buf[NSEQ][G::BUF];
-  for (int i = threadIdx.x; i < 32 * P; i += 256) s_twN[i] = A.twN[i];
+  __shared__ float s_gain[GLDS ? 2 * N : 1];
+  for (int i = threadIdx.x; i < NR * P; i += 256) s_twN[i] = A.twN[i];
   for (int i = threadIdx.x; i < P; i += 256) s_twP[i] = A.twP[i];
   for (int i = threadIdx.x; i < N; i += 256) s_win[i] = A.win[i];
+  if constexpr (GLDS) {
+    const int nr = A.n_rows_lds;
+    for (int i = threadIdx.x; i < nr * N; i += 256) s_gain[i] = A.gains[i];
+  }
   __syncthreads();
 
   const int seq = threadIdx.x / P, L = threadIdx.x % P;
-  const int run_id = blockIdx.x * NSEQ + seq;
+  // wave-uniform run id (readfirstlane: run and stream descriptors load as scalars)
+  const int run_id = __builtin_amdgcn_readfirstlane(blockIdx.x * NSEQ + seq);
   Run R{0, 0, 0, 0};
   const bool valid = run_id < A.n_runs;
   if (valid) R = A.runs[run_id];
@@ -529,7 +565,7 @@ __global__ __launch_bounds__(256) void k_stft_ola(MainArgs A) {
   const TomatisStream S = A.st[R.s];
   const int64_t kfirst = max<int64_t>(0, R.ka - (A.rmax - 1));
   int nit = valid ? (int)(R.kb - kfirst) : 0;
-  if constexpr (P > 64) {
+  if constexpr (P > 64) {  // the block's sequences share barriers: same trip count
     __shared__ int s_nit[NSEQ];
     if (L == 0) s_nit[seq] = nit;
     __syncthreads();
@@ -543,11 +579,6 @@ __global__ __launch_bounds__(256) void k_stft_ola(MainArgs A) {
   const int64_t out_end = S.out_begin + S.out_len;
   const float oscale = S.out_scale;
   const float iscale = S.in_scale;
-  const float* grows = A.gains;
-
-  float winv[SH];
-#pragma unroll
-  for (int i = 0; i < SH; ++i) winv[i] = A.winv[L + P * i];
 
   if (valid && R.ka == 0 && S.first_start > S.out_begin) {  // adaptive: zeros before frame 0
     for (int64_t p = S.out_begin + L; p < min(S.first_start, out_end); p += P)
@@ -563,48 +594,54 @@ __global__ __launch_bounds__(256) void k_stft_ola(MainArgs A) {
   const int64_t chunk_k_step = S.n_chunks > 1 ? S.chunk_len / HOP : 0;
   float pk = 0.f;
 
-  cf acc[32 - SH];
+  cf acc[NC];
 #pragma unroll
-  for (int i = 0; i < 32 - SH; ++i) acc[i] = {0.f, 0.f};
+  for (int i = 0; i < NC; ++i) acc[i] = {0.f, 0.f};
 
   for (int it = 0; it < nit; ++it) {
     const int64_t k = kfirst + it;
     const bool live = valid && (k < R.kb);
     const int64_t s_k = S.first_start + k * HOP;
-    cf v[32];
-    // ---- load + analysis window ----
-    const bool interior = (s_k >= 0) && (s_k + N <= S.n);
-    if (live && interior) {
-      const float* xf = xs + CH * s_k;
+    const uint16_t row = live ? A.rows[S.frame_base + k] : 0;
+    cf v[NR];
+    if (live && s_k >= 0 && s_k + N <= S.n) {
+      const __amdgpu_buffer_rsrc_t rx = mk_rsrc(xs + CH * s_k, N * CH * 4);
 #pragma unroll
-      for (int n2 = 0; n2 < 32; ++n2) v[n2] = load_cf<CH>(xf, L + P * n2);
+      for (int n2 = 0; n2 < NR; ++n2) v[n2] = bload<CH>(rx, L * CH * 4, P * n2 * CH * 4);
     } else {
 #pragma unroll
-      for (int n2 = 0; n2 < 32; ++n2) {
+      for (int n2 = 0; n2 < NR; ++n2) {
         const int64_t p = s_k + L + P * n2;
         v[n2] = (live && p >= 0 && p < S.n) ? load_cf<CH>(xs, p) : cf{0.f, 0.f};
       }
     }
-    const uint16_t row = live ? A.rows[S.frame_base + k] : 0;
-    if (iscale != 1.0f) {  // (x * scale) * win, two roundings as the reference
+    // ---- analysis window (x * in_scale first, two roundings as the reference) ----
+    if (iscale != 1.0f) {
 #pragma unroll
-      for (int n2 = 0; n2 < 32; ++n2) v[n2] = cscale(v[n2], iscale);
+      for (int n2 = 0; n2 < NR; ++n2) v[n2] = cscale(v[n2], iscale);
     }
 #pragma unroll
-    for (int n2 = 0; n2 < 32; ++n2) v[n2] = cscale(v[n2], s_win[L + P * n2]);
-    fft_fwd<P>(v, L, s_twN, s_twP, buf);
-    // ---- gain row (real, even, 1/N folded in), coalesced per-lane layout ----
-    {
-      const float* g = grows + (int64_t)row * N;
+    for (int n2 = 0; n2 < NR; ++n2) v[n2] = cscale(v[n2], s_win[L + P * n2]);
+    fft_fwd<P, NR>(v, L, s_twN, s_twP, buf);
+    // ---- gain row (real, even, 1/N folded in), per-lane layout ----
+    if constexpr (GLDS) {
+      const float* g = s_gain + (row ? N : 0);
 #pragma unroll
-      for (int i = 0; i < 32; ++i) v[i] = cscale(v[i], g[i * P + L]);
+      for (int i = 0; i < NR; ++i) v[i] = cscale(v[i], g[i * P + L]);
+    } else {
+      const __amdgpu_buffer_rsrc_t rg = mk_rsrc(A.gains + (int64_t)row * N, N * 4);
+#pragma unroll
+      for (int i = 0; i < NR; ++i) v[i] = cscale(v[i], bloadf(rg, L * 4, i * P * 4));
     }
-    fft_inv<P>(v, L, s_twN, s_twP, buf);
-    // ---- synthesis window + register OLA ----
+    fft_inv<P, NR>(v, L, s_twN, s_twP, buf);
+    // ---- synthesis window fused with the register OLA ----
 #pragma unroll
-    for (int n2 = 0; n2 < 32; ++n2) v[n2] = cscale(v[n2], s_win[L + P * n2]);
+    for (int i = 0; i < NC; ++i) {
+      const float w = s_win[L + P * i];
+      v[i] = {__builtin_fmaf(v[i].x, w, acc[i].x), __builtin_fmaf(v[i].y, w, acc[i].y)};
+    }
 #pragma unroll
-    for (int i = 0; i < 32 - SH; ++i) v[i] = v[i] + acc[i];
+    for (int i = NC; i < NR; ++i) v[i] = cscale(v[i], s_win[L + P * i]);
     if (live && k >= R.ka) {
       if (k == next_chunk_k) {
         flush_peak<P>(pk, cid, S, A.peaks, L);
@@ -614,11 +651,11 @@ __global__ __launch_bounds__(256) void k_stft_ola(MainArgs A) {
       const bool full = (s_k >= S.out_begin) && (s_k + HOP <= out_end);
       const bool edge = (k < A.rmax - 1);
       if (full && !edge) {
-        float* yb = ys + CH * (s_k - S.out_begin);
+        const __amdgpu_buffer_rsrc_t ry = mk_rsrc(ys + CH * (s_k - S.out_begin), HOP * CH * 4);
 #pragma unroll
         for (int i = 0; i < SH; ++i) {
-          const cf o = cscale(cscale(v[i], winv[i]), oscale);
-          store_cf<CH>(yb, L + P * i, o);
+          const cf o = cscale(cscale(v[i], A.winv[L + P * i]), oscale);
+          bstore<CH>(o, ry, L * CH * 4, P * i * CH * 4);
           pk = fmaxf(pk, cmag<CH>(o));
         }
       } else {
@@ -636,7 +673,7 @@ __global__ __launch_bounds__(256) void k_stft_ola(MainArgs A) {
       }
       if (R.last && k == R.kb - 1) {  // stream tail after the last frame
 #pragma unroll
-        for (int i = SH; i < 32; ++i) {
+        for (int i = SH; i < NR; ++i) {
           const int64_t p = s_k + L + P * i;
           if (p >= S.out_begin && p < out_end) {
             const float d = norm_den(wsum_rel(p - S.first_start, S.n_frames, HOP, N, A.win2),
@@ -649,22 +686,22 @@ __global__ __launch_bounds__(256) void k_stft_ola(MainArgs A) {
       }
     }
 #pragma unroll
-    for (int i = 0; i < 32 - SH; ++i) acc[i] = v[i + SH];
+    for (int i = 0; i < NC; ++i) acc[i] = v[i + SH];
   }
   if (valid) flush_peak<P>(pk, cid, S, A.peaks, L);
 }
 
 // Generic hop: same transform, windowed frame outputs to scratch, then a gather.
-template <int P>
-__global__ __launch_bounds__(256) void k_stft_frames(MainArgs A) {
-  using G = FftGeo<P>;
+template <int P, int NR>
+__global__ __launch_bounds__(256, 2) void k_stft_frames(MainArgs A) {
+  using G = FftGeo<P, NR>;
   constexpr int N = G::N;
   constexpr int NSEQ = 256 / P;
-  __shared__ cf s_twN[32 * P];
+  __shared__ cf s_twN[NR * P];
   __shared__ cf s_twP[P];
   __shared__ float s_win[N];
   __shared__ cf s_buf[NSEQ][G::BUF];
-  for (int i = threadIdx.x; i < 32 * P; i += 256) s_twN[i] = A.twN[i];
+  for (int i = threadIdx.x; i < NR * P; i += 256) s_twN[i] = A.twN[i];
   for (int i = threadIdx.x; i < P; i += 256) s_twP[i] = A.twP[i];
   for (int i = threadIdx.x; i < N; i += 256) s_win[i] = A.win[i];
   __syncthreads();
@@ -693,9 +730,9 @@ __global__ __launch_bounds__(256) void k_stft_frames(MainArgs A) {
     const int64_t k = R.ka + it;
     const bool live = valid && (k < R.kb);
     const int64_t s_k = S.first_start + k * hop;
-    cf v[32];
+    cf v[NR];
 #pragma unroll
-    for (int n2 = 0; n2 < 32; ++n2) {
+    for (int n2 = 0; n2 < NR; ++n2) {
       const int64_t p = s_k + L + P * n2;
       cf z = {0.f, 0.f};
       if (live && p >= 0 && p < S.n) {
@@ -705,31 +742,31 @@ __global__ __launch_bounds__(256) void k_stft_frames(MainArgs A) {
       const float w = s_win[L + P * n2];
       v[n2] = {(z.x * S.in_scale) * w, (z.y * S.in_scale) * w};
     }
-    fft_fwd<P>(v, L, s_twN, s_twP, buf);
+    fft_fwd<P, NR>(v, L, s_twN, s_twP, buf);
     const uint16_t row = live ? A.rows[S.frame_base + k] : 0;
     const float* g = A.gains + (int64_t)row * N;
 #pragma unroll
-    for (int i = 0; i < 32; ++i) v[i] = cscale(v[i], g[i * P + L]);
-    fft_inv<P>(v, L, s_twN, s_twP, buf);
+    for (int i = 0; i < NR; ++i) v[i] = cscale(v[i], g[i * P + L]);
+    fft_inv<P, NR>(v, L, s_twN, s_twP, buf);
     if (live) {
       cf* dst = A.scratch + (S.frame_base + k) * (int64_t)N;
 #pragma unroll
-      for (int n2 = 0; n2 < 32; ++n2) dst[L + P * n2] = cscale(v[n2], s_win[L + P * n2]);
+      for (int n2 = 0; n2 < NR; ++n2) dst[L + P * n2] = cscale(v[n2], s_win[L + P * n2]);
     }
   }
 }
 
 // gain rows [rows][n_bins] -> [rows][N] in the per-lane bin layout of fft_fwd,
 // mirrored (real even gain) and scaled by 1/N (exact: power of two)
-template <int P>
+template <int P, int NR>
 __global__ void k_gain_perm(const float* __restrict__ g, int n_rows, int n_bins,
                             float* __restrict__ out) {
-  constexpr int N = 32 * P;
+  constexpr int N = NR * P;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_rows * N) return;
   const int row = t / N, e = t - row * N;
   const int i = e / P, L = e - i * P;
-  int b = fft_bin<P>(L, i);
+  int b = fft_bin<P, NR>(L, i);
   b = (b <= N / 2) ? b : N - b;
   out[t] = g[(int64_t)row * n_bins + b] * (1.0f / (float)N);
 }
@@ -866,7 +903,7 @@ struct tomatis_plan_s {
   int32_t n_streams = 0;
   int64_t total_frames = 0;
   int32_t total_chunks = 0;
-  int P = 0, SH = 0, rmax = 1;
+  int P = 0, NR = 32, SH = 0, rmax = 1;
   bool generic = false;
   std::vector<TomatisStream> hs;
   int lvl_nf = 0;
@@ -926,10 +963,16 @@ int env_int(const char* name, int dflt) {
 
 int launch_check() { return hipfail(hipGetLastError()); }
 
-template <int P, int SH>
+template <int P, int NR, int SH>
 void launch_main(const MainArgs& A, int ch, int nseq_blocks, hipStream_t s) {
-  if (ch == 2) hipLaunchKernelGGL((k_stft_ola<P, SH, 2>), dim3(nseq_blocks), dim3(256), 0, s, A);
-  else hipLaunchKernelGGL((k_stft_ola<P, SH, 1>), dim3(nseq_blocks), dim3(256), 0, s, A);
+  const bool gl = A.n_rows_lds > 0;
+  if (ch == 2) {
+    if (gl) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, true>), dim3(nseq_blocks), dim3(256), 0, s, A);
+    else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, false>), dim3(nseq_blocks), dim3(256), 0, s, A);
+  } else {
+    if (gl) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, true>), dim3(nseq_blocks), dim3(256), 0, s, A);
+    else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, false>), dim3(nseq_blocks), dim3(256), 0, s, A);
+  }
 }
 
 }  // namespace
@@ -1053,8 +1096,9 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
       winv[m] = 1.0f / den;
     }
     p->rmax = (N + hop - 1) / hop;
-    std::vector<cf> twN((size_t)32 * P), twP(P);
-    for (int k2 = 0; k2 < 32; ++k2)
+    const int NRr = p->NR;
+    std::vector<cf> twN((size_t)NRr * P), twP(P);
+    for (int k2 = 0; k2 < NRr; ++k2)
       for (int n1 = 0; n1 < P; ++n1) {
         const double ang = -2.0 * M_PI * (double)((int64_t)n1 * k2 % N) / (double)N;
         twN[(size_t)k2 * P + n1] = {(float)cos(ang), (float)sin(ang)};
@@ -1138,9 +1182,12 @@ int tomatis_plan_create(tomatis_plan_t* out, const TomatisPlanDesc* desc, const 
   p->d = d;
   p->n_streams = n_streams;
   const int N = d.n_fft, hop = d.hop;
-  p->P = N / 32;
+  // (lanes P, registers NR) per transform: 2048 = 128 x 16, 4096 = 128 x 32
+  p->P = 128;
+  p->NR = N / 128;
   p->SH = (hop % p->P == 0) ? hop / p->P : 0;
-  p->generic = !(p->SH == 4 || p->SH == 8 || p->SH == 16);
+  p->generic = p->NR == 16 ? !(p->SH == 2 || p->SH == 4 || p->SH == 8)
+                           : !(p->SH == 4 || p->SH == 8 || p->SH == 16);
   for (int i = 0; i < n_streams && !p->generic; ++i) {
     const TomatisStream& s = streams[i];
     if (s.n_chunks > 1 && (((s.chunk_first - s.first_start) % hop) != 0 || (s.chunk_len % hop) != 0))
@@ -1278,10 +1325,10 @@ int tomatis_stft_ola(tomatis_plan_t p, const float* x, const float* gains, int32
     p->gperm_rows = n_rows;
   }
   const int nb = (n_rows * N + 255) / 256;
-  if (p->P == 64)
-    hipLaunchKernelGGL(k_gain_perm<64>, dim3(nb), dim3(256), 0, s, gains, n_rows, N / 2 + 1, p->gperm);
+  if (p->NR == 16)
+    hipLaunchKernelGGL((k_gain_perm<128, 16>), dim3(nb), dim3(256), 0, s, gains, n_rows, N / 2 + 1, p->gperm);
   else
-    hipLaunchKernelGGL(k_gain_perm<128>, dim3(nb), dim3(256), 0, s, gains, n_rows, N / 2 + 1, p->gperm);
+    hipLaunchKernelGGL((k_gain_perm<128, 32>), dim3(nb), dim3(256), 0, s, gains, n_rows, N / 2 + 1, p->gperm);
   MainArgs A;
   A.x = x;
   A.y = y;
@@ -1303,12 +1350,13 @@ int tomatis_stft_ola(tomatis_plan_t p, const float* x, const float* gains, int32
   A.norm_mode = p->d.norm_mode;
   A.rmax = p->generic ? 1 : p->rmax;
   A.inv_n = 1.0f / (float)N;
+  A.n_rows_lds = (n_rows <= 2 && p->NR == 16) ? n_rows : 0;
   const int nseq = 256 / p->P;
   const int blocks = (p->n_runs + nseq - 1) / nseq;
   const int ch = p->d.ch;
   if (p->generic) {
-    if (p->P == 64) hipLaunchKernelGGL(k_stft_frames<64>, dim3(blocks), dim3(256), 0, s, A);
-    else hipLaunchKernelGGL(k_stft_frames<128>, dim3(blocks), dim3(256), 0, s, A);
+    if (p->NR == 16) hipLaunchKernelGGL((k_stft_frames<128, 16>), dim3(blocks), dim3(256), 0, s, A);
+    else hipLaunchKernelGGL((k_stft_frames<128, 32>), dim3(blocks), dim3(256), 0, s, A);
     int rc = launch_check();
     if (rc || p->total_out == 0) return rc;
     const int64_t ng = (p->total_out + 255) / 256;
@@ -1316,14 +1364,14 @@ int tomatis_stft_ola(tomatis_plan_t p, const float* x, const float* gains, int32
                        p->pos_base, p->total_out, N);
     return launch_check();
   }
-  if (p->P == 64) {
-    if (p->SH == 4) launch_main<64, 4>(A, ch, blocks, s);
-    else if (p->SH == 8) launch_main<64, 8>(A, ch, blocks, s);
-    else launch_main<64, 16>(A, ch, blocks, s);
+  if (p->NR == 16) {
+    if (p->SH == 2) launch_main<128, 16, 2>(A, ch, blocks, s);
+    else if (p->SH == 4) launch_main<128, 16, 4>(A, ch, blocks, s);
+    else launch_main<128, 16, 8>(A, ch, blocks, s);
   } else {
-    if (p->SH == 4) launch_main<128, 4>(A, ch, blocks, s);
-    else if (p->SH == 8) launch_main<128, 8>(A, ch, blocks, s);
-    else launch_main<128, 16>(A, ch, blocks, s);
+    if (p->SH == 4) launch_main<128, 32, 4>(A, ch, blocks, s);
+    else if (p->SH == 8) launch_main<128, 32, 8>(A, ch, blocks, s);
+    else launch_main<128, 32, 16>(A, ch, blocks, s);
   }
   return launch_check();
 }
