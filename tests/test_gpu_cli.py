@@ -1,0 +1,147 @@
+"""GPU end-to-end: the drop-in CLIs (file -> file) and the batch runner.
+
+Outputs go through the WAV PCM_24 fallback (no libsndfile in the image), so the
+sample tolerance is 1e-4 plus one 24-bit LSB.  State CSVs are compared as text
+with the CSV the reference would write for the same frames (levels / states
+from the oracle, which is bit-exact with the reference, formatted like the
+reference).
+"""
+import csv
+import io
+import os
+
+import numpy as np
+import pytest
+
+from oracle import tomatis_oracle as orc
+from tomatis_audio_processor_amd import audio_io
+from tomatis_audio_processor_amd.synth import synth_stream
+
+pytestmark = pytest.mark.gpu
+LSB = 1.0 / 8388607
+
+
+def _gpu():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _wav(tmp_path, name, x, sr):
+    p = str(tmp_path / name)
+    audio_io.write(p, x, sr, "WAV", "FLOAT")
+    return p
+
+
+def _cmp(y, ref, mask, tol=1e-4 + LSB):
+    err = np.abs(np.asarray(y, np.float64) - np.asarray(ref, np.float64))[mask]
+    assert float(err.max(initial=0)) <= tol, float(err.max())
+
+
+def test_process_tomatis_cli(tmp_path):
+    _gpu()
+    from tomatis_audio_processor_amd import process_tomatis
+    sr, N = 48000, 48000 * 6 + 123
+    x = synth_stream(101, N, 2, sr)
+    inp = _wav(tmp_path, "in.wav", x, sr)
+    out = str(tmp_path / "out.flac")
+    st_csv = str(tmp_path / "st.csv")
+    rc = process_tomatis.main(["-i", inp, "-o", out, "--n_fft", "2048", "--hop", "512",
+                               "--state_csv", st_csv])
+    assert rc == 0
+    y, sr2 = audio_io.read(out.replace(".flac", ".wav"))
+    ref = orc.process_standard(x, sr, gate_ui=50, n_fft=2048, hop=512)
+    m = (ref["wsum"][ref["pad"]:ref["pad"] + N] >= 1e-3)
+    _cmp(y, ref["y"], m)
+    # state CSV text as the reference writes it (csv module, repr floats)
+    buf = io.StringIO(newline="")
+    w = csv.writer(buf)
+    w.writerow(["frame_idx", "time_sec", "level_dbfs", "state"])
+    for k in np.nonzero((ref["starts"] >= 0) & (ref["starts"] < N))[0]:
+        w.writerow([int(k), int(ref["starts"][k]) / sr, float(ref["levels"][k]),
+                    "C1" if ref["states"][k] == 1 else "C2"])
+    assert open(st_csv, newline="", encoding="utf-8").read() == buf.getvalue()
+
+
+def test_process_tomatis_guard(tmp_path):
+    _gpu()
+    from tomatis_audio_processor_amd import process_tomatis
+    x = synth_stream(102, 44100, 2, 44100)
+    inp = _wav(tmp_path, "in44.wav", x, 44100)
+    assert process_tomatis.main(["-i", inp, "-o", str(tmp_path / "o.flac")]) == 1
+    assert process_tomatis.main(["-i", inp, "-o", str(tmp_path / "o.flac"), "--n_fft", "2048",
+                                 "--hop", "512", "--allow_any_format"]) == 0
+
+
+def test_xfade_and_adaptive_cli(tmp_path):
+    _gpu()
+    from tomatis_audio_processor_amd import process_tomatis_xfade, process_tomatis_adaptive
+    sr, N = 48000, 48000 * 5
+    x = synth_stream(103, N, 2, sr)
+    inp = _wav(tmp_path, "in.wav", x, sr)
+    out = str(tmp_path / "xf.wav")
+    assert process_tomatis_xfade.main(["-i", inp, "-o", out, "--gate_offset", "-90",
+                                       "--xfade_ms", "500", "--n_fft", "2048", "--hop", "512",
+                                       "--state_csv", str(tmp_path / "xf.csv")]) == 0
+    ref = orc.process_standard(x, sr, gate_ui=50, gate_offset=-90, n_fft=2048, hop=512,
+                               xfade_ms=500.0)
+    y, _ = audio_io.read(out)
+    _cmp(y, ref["y"], ref["wsum"][ref["pad"]:ref["pad"] + N] >= 1e-3)
+    rows = list(csv.reader(open(tmp_path / "xf.csv", newline="", encoding="utf-8")))[1:]
+    m = (ref["starts"] >= 0) & (ref["starts"] < N)
+    assert [r[4] for r in rows] == [f"{a:.3f}" for a in ref["alpha"][m]]
+    assert [r[2] for r in rows] == [f"{v:.2f}" for v in ref["levels"][m]]
+    out2 = str(tmp_path / "ad.wav")
+    assert process_tomatis_adaptive.main(["-i", inp, "-o", out2, "--n_fft", "2048", "--hop",
+                                          "512", "--state_csv", str(tmp_path / "ad.csv")]) == 0
+    ra = orc.process_adaptive(x, sr, n_fft=2048, hop=512)
+    y2, _ = audio_io.read(out2)
+    _cmp(y2, ra["y"], ra["wsum"] >= 1e-3)
+    rows = list(csv.reader(open(tmp_path / "ad.csv", newline="", encoding="utf-8")))[1:]
+    assert [r[3] for r in rows] == ["C1" if s == 1 else "C2" for s in ra["states"]]
+    assert [r[4] for r in rows] == [f"{a:.4f}" for a in ra["alpha"]]
+
+
+def test_layer2_cli_gain_protect(tmp_path):
+    _gpu()
+    from tomatis_audio_processor_amd import layer2_apply_eq
+    from tests.golden.cases import eq_csv_rows
+    from tests.golden_util import parse_eq_csv
+    sr, N = 48000, 100000
+    x = synth_stream(104, N, 2, sr)
+    inp = _wav(tmp_path, "in.wav", x, sr)
+    eq = str(tmp_path / "eq.csv")
+    open(eq, "w").write(eq_csv_rows())
+    out = str(tmp_path / "l2.flac")
+    layer2_apply_eq.main(["-i", inp, "-o", out, "--eq_csv", eq, "--n_fft", "2048", "--hop", "512"])
+    fr, db = parse_eq_csv(eq_csv_rows())
+    ref = orc.apply_eq_stft(x, sr, fr, db, n_fft=2048, hop=512)
+    y, _ = audio_io.read(out.replace(".flac", ".wav"))
+    assert y.shape == ref["y"].shape
+    # PCM_24 clips the reference's ill-conditioned head samples (F7): compare the rest
+    m = (ref["wsum"] >= 1e-3)[:, None] & (np.abs(ref["y"]) < 0.99)
+    _cmp(y, ref["y"], m)
+    if ref["y_gp"] is not None:
+        assert os.path.exists(out.replace(".flac", "_gp.wav"))
+
+
+def test_batch_runner_single_process(tmp_path):
+    _gpu()
+    from tomatis_audio_processor_amd import batch
+    import json
+    sr = 48000
+    files = []
+    for i in range(3):
+        x = synth_stream(200 + i, sr * (2 + i), 2, sr)
+        files.append(_wav(tmp_path, f"f{i}.wav", x, sr))
+    od = str(tmp_path / "out")
+    assert batch.main(["-i", *files, "--out_dir", od, "--n_fft", "2048", "--hop", "512"]) == 0
+    man = json.load(open(os.path.join(od, "manifest.json")))
+    assert [s["stream"] for s in man["streams"]] == [0, 1, 2]
+    for i in range(3):
+        x = synth_stream(200 + i, sr * (2 + i), 2, sr)
+        ref = orc.process_standard(x, sr, gate_ui=50, n_fft=2048, hop=512)
+        y, _ = audio_io.read(os.path.join(od, f"f{i}_tomatis.wav"))
+        N = len(x)
+        _cmp(y, ref["y"], ref["wsum"][ref["pad"]:ref["pad"] + N] >= 1e-3)
+        assert man["streams"][i]["c2_frames"] == int(np.count_nonzero(ref["states"] == 2))

@@ -1,0 +1,102 @@
+"""Multi-file, multi-GPU batch processing (file-parallel).
+
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+        --master-addr 127.0.0.1 -m tomatis_audio_processor_amd.batch \
+        --mode standard --out_dir out/ -i a.wav b.wav ...
+
+Every rank reads the headers of all inputs, takes its LPT shard
+(``sharding.lpt_partition`` on frames*channels), processes the shard as one
+batched stream set per (sr, ch) format on its own GPU, writes its outputs, and
+contributes fixed-size manifest records to one all_gather (RCCL over xGMI).
+Rank 0 writes ``manifest.json``.  Single-process runs need no launcher.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+from collections import defaultdict
+
+import numpy as np
+
+from . import audio_io, sharding
+
+
+def _dist():
+    import torch
+    import torch.distributed as dist
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+    if ws > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        dist.init_process_group(backend=backend, rank=rank, world_size=ws)
+    return rank, ws
+
+
+def run(args):
+    import torch
+    from . import engine
+    rank, ws = _dist()
+    infos = [audio_io.info(p) for p in args.input]
+    costs = [fr * ch for (sr, ch, fr) in infos]
+    mine = sharding.lpt_partition(costs, ws)[rank]
+    groups = defaultdict(list)
+    for i in mine:
+        groups[(infos[i][0], infos[i][1])].append(i)
+    os.makedirs(args.out_dir, exist_ok=True)
+    recs = []
+    params = dict(n_fft=args.n_fft, hop=args.hop)
+    for (sr, ch), ids in sorted(groups.items()):
+        xs = [audio_io.read(args.input[i])[0] for i in ids]
+        ss = engine.StreamSet.from_arrays(xs, sr)
+        if args.mode == "adaptive":
+            pipe = engine.AdaptivePipeline(ss, **params)
+        elif args.mode == "xfade":
+            pipe = engine.GatePipeline(ss, gate_ui=args.gate_ui, gate_offset=args.gate_offset,
+                                       xfade_ms=args.xfade_ms, **params)
+        else:
+            pipe = engine.GatePipeline(ss, gate_ui=args.gate_ui, gate_mode=args.gate_mode,
+                                       gate_offset=args.gate_offset, **params)
+        res = pipe.run()
+        torch.cuda.synchronize()
+        for j, i in enumerate(ids):
+            base = os.path.splitext(os.path.basename(args.input[i]))[0]
+            out = os.path.join(args.out_dir, f"{base}_tomatis.{args.out_ext}")
+            if args.out_ext == "wav":
+                audio_io.write(out, res.output(j), sr, "WAV", "PCM_24")
+            else:
+                audio_io.write_with_fallback(out, res.output(j), sr, log=lambda m: None)
+        recs.append(sharding.stream_records(res, ids, rank))
+    rec = np.concatenate(recs) if recs else np.zeros((0, sharding.REC), np.int64)
+    dev = "cuda" if (ws > 1 and torch.cuda.is_available()) else None
+    allrec = sharding.gather_manifest(rec, device=dev)
+    if rank == 0:
+        man = [dict(zip(sharding.MANIFEST_FIELDS, map(int, r)), path=args.input[int(r[0])])
+               for r in allrec]
+        with open(os.path.join(args.out_dir, "manifest.json"), "w") as f:
+            json.dump({"world_size": ws, "streams": man}, f, indent=1)
+        print(f"[DONE] {len(man)} streams on {ws} GPU(s) -> {args.out_dir}/manifest.json")
+    return 0
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="Batch Tomatis processing on 1..8 MI355X")
+    ap.add_argument("-i", "--input", nargs="+", required=True)
+    ap.add_argument("--out_dir", required=True)
+    ap.add_argument("--mode", choices=["standard", "xfade", "adaptive"], default="standard")
+    ap.add_argument("--gate_ui", type=float, default=50)
+    ap.add_argument("--gate_mode", choices=["linear", "log_percent"], default="log_percent")
+    ap.add_argument("--gate_offset", type=float, default=-100)
+    ap.add_argument("--xfade_ms", type=float, default=500.0)
+    ap.add_argument("--n_fft", type=int, default=4096)
+    ap.add_argument("--hop", type=int, default=2048)
+    ap.add_argument("--out_ext", choices=["wav", "flac"], default="wav")
+    return run(ap.parse_args(argv))
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
