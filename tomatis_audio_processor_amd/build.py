@@ -12,7 +12,7 @@ DEPS = [SRC, os.path.join(HERE, "csrc", "tm_common.h"), os.path.join(HERE, "csrc
         os.path.join(ROOT, "include", "tomatis_hip.h")]
 OUT = os.path.join(HERE, "libtomatis_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "-fPIC", "-shared",
          "-I" + os.path.join(ROOT, "include")]
 
 

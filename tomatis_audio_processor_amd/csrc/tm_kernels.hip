@@ -164,6 +164,95 @@ __global__ __launch_bounds__(256) void k_levels(const float* __restrict__ x,
   }
 }
 
+// ---------------------------------------------------------------------------
+// Streaming levels (hop % 128 == 0): numpy's pairwise mean over a power-of-two
+// frame is a perfect binary tree over 128-sample leaves aligned to the frame
+// start, so every 128-sample block (aligned to first_start) has ONE leaf sum
+// shared by all frames covering it.  k_leaves: lane = (block b, accumulator
+// chain c) over 8 blocks per wave; chain c sums m^2 of samples c, c+8, ..c+120
+// in order (numpy's 8 accumulators); the 8 chains combine as
+// ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) via xor-shuffles (IEEE add commutes).
+// k_frame_r: per frame, perfect-tree sum of n_fft/128 leaves, mean, sqrt.
+// ---------------------------------------------------------------------------
+template <typename T, int CH>
+__global__ __launch_bounds__(256) void k_leaves(const float* __restrict__ x,
+                                                const TomatisStream* __restrict__ st,
+                                                int n_streams,
+                                                const int64_t* __restrict__ grp_base,
+                                                const int64_t* __restrict__ leaf_base,
+                                                int64_t n_groups, T* __restrict__ leaves) {
+  const int lane = threadIdx.x & 63;
+  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // 8-block group
+  if (g >= n_groups) return;
+  int lo = 0, hi = n_streams - 1;  // stream of this group (wave-uniform)
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (grp_base[mid] <= g) lo = mid;
+    else hi = mid - 1;
+  }
+  const TomatisStream S = st[lo];
+  const int64_t gl = g - grp_base[lo];
+  const int b = lane >> 3, c = lane & 7;
+  const int64_t blk = gl * 8 + b;
+  const int64_t nblk = leaf_base[lo + 1] - leaf_base[lo];
+  const int64_t p0 = S.first_start + gl * 1024;  // first sample of the group
+  const T scale = (T)S.in_scale;
+  const float* xs = x + S.in_off;
+  T acc = (T)0;
+  if (p0 >= 0 && p0 + 1024 <= S.n) {
+    T m2[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int64_t p = p0 + 128 * b + c + 8 * t;
+      if constexpr (CH == 2) {
+        const float2 u = reinterpret_cast<const float2*>(xs)[p];
+        const float v[2] = {u.x, u.y};
+        m2[t] = msq_of<T>(v, 2, scale);
+      } else {
+        m2[t] = msq_of<T>(xs + p, 1, scale);
+      }
+    }
+    acc = m2[0];
+#pragma unroll
+    for (int t = 1; t < 16; ++t) acc = acc + m2[t];
+  } else {
+    for (int t = 0; t < 16; ++t) {
+      const int64_t p = p0 + 128 * b + c + 8 * t;
+      const T m = (p >= 0 && p < S.n) ? msq_of<T>(xs + p * CH, CH, scale) : (T)0;
+      acc = (t == 0) ? m : acc + m;
+    }
+  }
+  // pairwise tree over the 8 chains of a block
+  acc = acc + __shfl_xor(acc, 1, 64);
+  acc = acc + __shfl_xor(acc, 2, 64);
+  acc = acc + __shfl_xor(acc, 4, 64);
+  if (c == 0 && blk < nblk) leaves[leaf_base[lo] + blk] = acc;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_frame_r(const TomatisStream* __restrict__ st,
+                                                 int n_streams, const int64_t* __restrict__ leaf_base,
+                                                 const T* __restrict__ leaves, int n_fft, int hop,
+                                                 int64_t total_frames, T* __restrict__ r_out) {
+  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= total_frames) return;
+  int lo = 0, hi = n_streams - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (st[mid].frame_base <= f) lo = mid;
+    else hi = mid - 1;
+  }
+  const int64_t k = f - st[lo].frame_base;
+  const T* lv = leaves + leaf_base[lo] + k * (hop >> 7);
+  const int nleaf = n_fft >> 7;  // 16 or 32
+  T t[32];
+  for (int i = 0; i < nleaf; ++i) t[i] = lv[i];
+  for (int w = nleaf; w > 1; w >>= 1)
+    for (int i = 0; i < w / 2; ++i) t[i] = t[2 * i] + t[2 * i + 1];
+  const T mean = t[0] / (T)n_fft;
+  r_out[f] = sqrt(mean + (T)(sizeof(T) == 4 ? (double)kEps32 : kEps64));
+}
+
 // ===========================================================================
 // Standard gate (process_tomatis.py:373-385) as a transfer-function scan.
 // state id: 0 = C1 idle, 1..D = C1 pending for (id-1) frames, D+1 = C2.
@@ -532,7 +621,7 @@ __device__ __forceinline__ float bloadf(__amdgpu_buffer_rsrc_t r, int voff, int 
 // holds stream position s_k + L + P*i; the OLA accumulator for the next frame
 // is this frame's registers shifted by SH = hop/P.
 // GLDS: the (<= 2) gain rows live in LDS in the per-lane layout.
-template <int P, int NR, int SH, int CH, bool GLDS>
+template <int P, int NR, int SH, int CH, bool GLDS, bool PF>
 __global__ __launch_bounds__(256, 2) void k_stft_ola(MainArgs A) {
   using G = FftGeo<P, NR>;
   constexpr int N = G::N;
@@ -598,22 +687,38 @@ __global__ __launch_bounds__(256, 2) void k_stft_ola(MainArgs A) {
 #pragma unroll
   for (int i = 0; i < NC; ++i) acc[i] = {0.f, 0.f};
 
+  // frame loads are software-pipelined one frame ahead (the next frame's HBM/L2
+  // latency hides behind this frame's transforms)
+  auto load_frame = [&](int64_t kk, cf (&dst)[NR]) {
+    const bool lv = valid && (kk < R.kb);
+    const int64_t sk = S.first_start + kk * HOP;
+    if (lv && sk >= 0 && sk + N <= S.n) {
+      const __amdgpu_buffer_rsrc_t rx = mk_rsrc(xs + CH * sk, N * CH * 4);
+#pragma unroll
+      for (int n2 = 0; n2 < NR; ++n2) dst[n2] = bload<CH>(rx, L * CH * 4, P * n2 * CH * 4);
+    } else {
+#pragma unroll
+      for (int n2 = 0; n2 < NR; ++n2) {
+        const int64_t p = sk + L + P * n2;
+        dst[n2] = (lv && p >= 0 && p < S.n) ? load_cf<CH>(xs, p) : cf{0.f, 0.f};
+      }
+    }
+  };
+  cf nx[NR];
+  if constexpr (PF) load_frame(kfirst, nx);
+
   for (int it = 0; it < nit; ++it) {
     const int64_t k = kfirst + it;
     const bool live = valid && (k < R.kb);
     const int64_t s_k = S.first_start + k * HOP;
     const uint16_t row = live ? A.rows[S.frame_base + k] : 0;
     cf v[NR];
-    if (live && s_k >= 0 && s_k + N <= S.n) {
-      const __amdgpu_buffer_rsrc_t rx = mk_rsrc(xs + CH * s_k, N * CH * 4);
+    if constexpr (PF) {
 #pragma unroll
-      for (int n2 = 0; n2 < NR; ++n2) v[n2] = bload<CH>(rx, L * CH * 4, P * n2 * CH * 4);
+      for (int n2 = 0; n2 < NR; ++n2) v[n2] = nx[n2];
+      if (it + 1 < nit) load_frame(k + 1, nx);
     } else {
-#pragma unroll
-      for (int n2 = 0; n2 < NR; ++n2) {
-        const int64_t p = s_k + L + P * n2;
-        v[n2] = (live && p >= 0 && p < S.n) ? load_cf<CH>(xs, p) : cf{0.f, 0.f};
-      }
+      load_frame(k, v);
     }
     // ---- analysis window (x * in_scale first, two roundings as the reference) ----
     if (iscale != 1.0f) {
@@ -935,6 +1040,12 @@ struct tomatis_plan_s {
   int64_t* mh_off = nullptr;
   float* gperm = nullptr;
   int gperm_rows = 0;
+  // streaming levels (hop % 128 == 0): per-stream 8-block groups and leaves
+  bool leaf_path = false;
+  int64_t n_groups = 0;
+  int64_t* grp_base = nullptr;
+  int64_t* leaf_base = nullptr;
+  void* leaves = nullptr;
 };
 
 namespace {
@@ -963,16 +1074,23 @@ int env_int(const char* name, int dflt) {
 
 int launch_check() { return hipfail(hipGetLastError()); }
 
-template <int P, int NR, int SH>
-void launch_main(const MainArgs& A, int ch, int nseq_blocks, hipStream_t s) {
+template <int P, int NR, int SH, bool PF>
+void launch_main_pf(const MainArgs& A, int ch, int nseq_blocks, hipStream_t s) {
   const bool gl = A.n_rows_lds > 0;
   if (ch == 2) {
-    if (gl) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, true>), dim3(nseq_blocks), dim3(256), 0, s, A);
-    else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, false>), dim3(nseq_blocks), dim3(256), 0, s, A);
+    if (gl) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, true, PF>), dim3(nseq_blocks), dim3(256), 0, s, A);
+    else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, false, PF>), dim3(nseq_blocks), dim3(256), 0, s, A);
   } else {
-    if (gl) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, true>), dim3(nseq_blocks), dim3(256), 0, s, A);
-    else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, false>), dim3(nseq_blocks), dim3(256), 0, s, A);
+    if (gl) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, true, PF>), dim3(nseq_blocks), dim3(256), 0, s, A);
+    else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, false, PF>), dim3(nseq_blocks), dim3(256), 0, s, A);
   }
+}
+template <int P, int NR, int SH>
+void launch_main(const MainArgs& A, int ch, int nseq_blocks, hipStream_t s) {
+  // frame prefetch pays for NR = 16 (2 waves/SIMD kept); NR = 32 is register-bound
+  static const int pf = env_int("TOMATIS_PREFETCH", NR == 16 ? 1 : 0);
+  if (pf) launch_main_pf<P, NR, SH, NR == 16>(A, ch, nseq_blocks, s);
+  else launch_main_pf<P, NR, SH, false>(A, ch, nseq_blocks, s);
 }
 
 }  // namespace
@@ -996,7 +1114,8 @@ int tomatis_plan_destroy(tomatis_plan_t p) {
   if (!p) return TOMATIS_OK;
   void* ptrs[] = {p->st, p->runs, p->lblocks, p->segs, p->seg_first, p->seg_count, p->tf,
                   p->seg_start, p->win, p->win2, p->winv, p->twN, p->twP, p->scratch,
-                  p->pos_base, p->chunks, p->mh_tf, p->mh_cnt, p->mh_off, p->gperm};
+                  p->pos_base, p->chunks, p->mh_tf, p->mh_cnt, p->mh_off, p->gperm,
+                  p->grp_base, p->leaf_base, p->leaves};
   for (void* q : ptrs) dfree(q);
   delete p;
   return TOMATIS_OK;
@@ -1016,7 +1135,7 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
   const int64_t tf_total = std::max<int64_t>(1, p->total_frames);
   int T = env_int("TOMATIS_RUN_FRAMES", 0);
   if (T <= 0) {
-    const int64_t target = (P == 64) ? 8192 : 4096;
+    const int64_t target = 4096;
     T = (int)std::max<int64_t>(48, (tf_total + target - 1) / target);
   }
   std::vector<Run> runs;
@@ -1053,6 +1172,23 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
     }
     p->n_lblocks = (int)lb.size();
     if ((rc = dalloc_copy(&p->lblocks, lb))) return rc;
+  }
+  // --- streaming levels: leaves of 128 samples aligned to first_start ---
+  p->leaf_path = (hop % 128 == 0) && N >= 256 && N <= 4096 && (N & (N - 1)) == 0 &&
+                 (d.ch == 1 || d.ch == 2) && env_int("TOMATIS_LEVELS_LEGACY", 0) == 0;
+  if (p->leaf_path) {
+    std::vector<int64_t> gb(ns + 1, 0), lbase(ns + 1, 0);
+    for (int s = 0; s < ns; ++s) {
+      const int64_t F = p->hs[s].n_frames;
+      const int64_t nblk = F > 0 ? ((F - 1) * hop + N) / 128 : 0;
+      lbase[s + 1] = lbase[s] + nblk;
+      gb[s + 1] = gb[s] + (nblk + 7) / 8;
+    }
+    p->n_groups = gb[ns];
+    if ((rc = dalloc_copy(&p->grp_base, gb))) return rc;
+    if ((rc = dalloc_copy(&p->leaf_base, lbase))) return rc;
+    if (hipMalloc(&p->leaves, (size_t)std::max<int64_t>(1, lbase[ns]) * sizeof(double)))
+      return TOMATIS_E_NOMEM;
   }
   // --- gate segments ---
   {
@@ -1183,8 +1319,10 @@ int tomatis_plan_create(tomatis_plan_t* out, const TomatisPlanDesc* desc, const 
   p->n_streams = n_streams;
   const int N = d.n_fft, hop = d.hop;
   // (lanes P, registers NR) per transform: 2048 = 128 x 16, 4096 = 128 x 32
-  p->P = 128;
-  p->NR = N / 128;
+  // n_fft 2048: one wave per frame (P = 64, 32 registers, wave-local exchanges)
+  // unless TOMATIS_P64=0; otherwise two waves per frame (P = 128)
+  p->P = (N == 2048 && env_int("TOMATIS_P64", 1)) ? 64 : 128;
+  p->NR = N / p->P;
   p->SH = (hop % p->P == 0) ? hop / p->P : 0;
   p->generic = p->NR == 16 ? !(p->SH == 2 || p->SH == 4 || p->SH == 8)
                            : !(p->SH == 4 || p->SH == 8 || p->SH == 16);
@@ -1240,6 +1378,33 @@ int tomatis_levels(tomatis_plan_t p, const float* x, void* r_out, int32_t prec, 
   if (!p || !x || !r_out) return TOMATIS_E_ARG;
   if (p->n_lblocks == 0) return TOMATIS_OK;
   hipStream_t s = (hipStream_t)hs;
+  if (p->leaf_path && (prec == TOMATIS_F32 || prec == TOMATIS_F64)) {
+    const unsigned gblk = (unsigned)((p->n_groups + 3) / 4);
+    const unsigned fblk = (unsigned)((p->total_frames + 255) / 256);
+    const int ch = p->d.ch, N = p->d.n_fft, hop = p->d.hop, ns = p->n_streams;
+    if (prec == TOMATIS_F32) {
+      float* lv = (float*)p->leaves;
+      if (ch == 2)
+        hipLaunchKernelGGL((k_leaves<float, 2>), dim3(gblk), dim3(256), 0, s, x, p->st, ns,
+                           p->grp_base, p->leaf_base, p->n_groups, lv);
+      else
+        hipLaunchKernelGGL((k_leaves<float, 1>), dim3(gblk), dim3(256), 0, s, x, p->st, ns,
+                           p->grp_base, p->leaf_base, p->n_groups, lv);
+      hipLaunchKernelGGL(k_frame_r<float>, dim3(fblk), dim3(256), 0, s, p->st, ns, p->leaf_base,
+                         lv, N, hop, p->total_frames, (float*)r_out);
+    } else {
+      double* lv = (double*)p->leaves;
+      if (ch == 2)
+        hipLaunchKernelGGL((k_leaves<double, 2>), dim3(gblk), dim3(256), 0, s, x, p->st, ns,
+                           p->grp_base, p->leaf_base, p->n_groups, lv);
+      else
+        hipLaunchKernelGGL((k_leaves<double, 1>), dim3(gblk), dim3(256), 0, s, x, p->st, ns,
+                           p->grp_base, p->leaf_base, p->n_groups, lv);
+      hipLaunchKernelGGL(k_frame_r<double>, dim3(fblk), dim3(256), 0, s, p->st, ns, p->leaf_base,
+                         lv, N, hop, p->total_frames, (double*)r_out);
+    }
+    return launch_check();
+  }
   if (prec == TOMATIS_F32) {
     hipLaunchKernelGGL((k_levels<float, true>), dim3(p->n_lblocks), dim3(256), 0, s, x, p->st,
                        p->lblocks, p->d.n_fft, p->d.hop, p->d.ch, (float*)r_out);
@@ -1325,7 +1490,9 @@ int tomatis_stft_ola(tomatis_plan_t p, const float* x, const float* gains, int32
     p->gperm_rows = n_rows;
   }
   const int nb = (n_rows * N + 255) / 256;
-  if (p->NR == 16)
+  if (p->P == 64)
+    hipLaunchKernelGGL((k_gain_perm<64, 32>), dim3(nb), dim3(256), 0, s, gains, n_rows, N / 2 + 1, p->gperm);
+  else if (p->NR == 16)
     hipLaunchKernelGGL((k_gain_perm<128, 16>), dim3(nb), dim3(256), 0, s, gains, n_rows, N / 2 + 1, p->gperm);
   else
     hipLaunchKernelGGL((k_gain_perm<128, 32>), dim3(nb), dim3(256), 0, s, gains, n_rows, N / 2 + 1, p->gperm);
@@ -1350,12 +1517,13 @@ int tomatis_stft_ola(tomatis_plan_t p, const float* x, const float* gains, int32
   A.norm_mode = p->d.norm_mode;
   A.rmax = p->generic ? 1 : p->rmax;
   A.inv_n = 1.0f / (float)N;
-  A.n_rows_lds = (n_rows <= 2 && p->NR == 16) ? n_rows : 0;
+  A.n_rows_lds = (n_rows <= 2 && N <= 2048) ? n_rows : 0;
   const int nseq = 256 / p->P;
   const int blocks = (p->n_runs + nseq - 1) / nseq;
   const int ch = p->d.ch;
   if (p->generic) {
-    if (p->NR == 16) hipLaunchKernelGGL((k_stft_frames<128, 16>), dim3(blocks), dim3(256), 0, s, A);
+    if (p->P == 64) hipLaunchKernelGGL((k_stft_frames<64, 32>), dim3(blocks), dim3(256), 0, s, A);
+    else if (p->NR == 16) hipLaunchKernelGGL((k_stft_frames<128, 16>), dim3(blocks), dim3(256), 0, s, A);
     else hipLaunchKernelGGL((k_stft_frames<128, 32>), dim3(blocks), dim3(256), 0, s, A);
     int rc = launch_check();
     if (rc || p->total_out == 0) return rc;
@@ -1364,7 +1532,11 @@ int tomatis_stft_ola(tomatis_plan_t p, const float* x, const float* gains, int32
                        p->pos_base, p->total_out, N);
     return launch_check();
   }
-  if (p->NR == 16) {
+  if (p->P == 64) {
+    if (p->SH == 4) launch_main<64, 32, 4>(A, ch, blocks, s);
+    else if (p->SH == 8) launch_main<64, 32, 8>(A, ch, blocks, s);
+    else launch_main<64, 32, 16>(A, ch, blocks, s);
+  } else if (p->NR == 16) {
     if (p->SH == 2) launch_main<128, 16, 2>(A, ch, blocks, s);
     else if (p->SH == 4) launch_main<128, 16, 4>(A, ch, blocks, s);
     else launch_main<128, 16, 8>(A, ch, blocks, s);
