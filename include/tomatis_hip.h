@@ -25,7 +25,8 @@
  *   src/process_tomatis_adaptive.py:298-338      tomatis_stft_ola
  *   src/layer2_apply_eq.py:143-214               tomatis_stft_ola
  *   src/layer2b_apply_residual_eq.py:120-160     tomatis_stft_ola
- *   src/process_tomatis.py:331-357 (limiter),    tomatis_apply_limiter
+ *   src/process_tomatis.py:331-357 (limiter),    tomatis_apply_limiter,
+ *                                                 tomatis_stft_ola_limited
  *   src/process_tomatis_adaptive.py:340-345
  *   np.max(np.abs(x)) (adaptive :201,          tomatis_absmax
  *       layer2 gain protect :178,213)
@@ -46,7 +47,7 @@
 extern "C" {
 #endif
 
-#define TOMATIS_ABI_VERSION 1
+#define TOMATIS_ABI_VERSION 2
 
 #define TOMATIS_OK 0
 #define TOMATIS_E_ARG (-1)        /* bad argument */
@@ -158,6 +159,18 @@ int tomatis_stft_ola(tomatis_plan_t plan, const float* x, const float* gain_rows
  * (float32 division, as the reference) when peak_j > limit. */
 int tomatis_apply_limiter(tomatis_plan_t plan, float* y, const uint32_t* chunk_peak_bits,
                           float limit, void* hip_stream);
+
+/* tomatis_stft_ola followed by tomatis_apply_limiter(limit), with the limiter
+ * done inside the transform kernel when every chunk's samples come from a few
+ * neighbouring runs (each wave rescales its own samples once its chunks are
+ * complete); otherwise the two launches.  Same results as the pair. */
+int tomatis_stft_ola_limited(tomatis_plan_t plan, const float* x, const float* gain_rows,
+                             int32_t n_rows, const uint16_t* rows, float* y,
+                             uint32_t* chunk_peak_bits, float limit, void* hip_stream);
+
+/* Synchronous: TOMATIS_E_HIP if a device-side consistency check of the plan's
+ * kernels has fired since creation (fused-limiter wait bound), else OK. */
+int tomatis_plan_error(tomatis_plan_t plan, void* hip_stream);
 
 /* max |x| over n floats as float bits (out zeroed by caller). */
 int tomatis_absmax(const float* x, int64_t n, uint32_t* out_bits, void* hip_stream);

@@ -36,6 +36,7 @@ def test_fullsize_standard(secs, sr, n_fft, hop):
     pipe = E.GatePipeline(ss, gate_ui=50, n_fft=n_fft, hop=hop)
     res = pipe.run()
     torch.cuda.synchronize()
+    pipe.plan.check_device()  # fused-limiter waits all completed
     rng = np.random.default_rng(secs)
     # input generator parity on sampled windows
     for a in rng.integers(0, n - 4096, 4):

@@ -126,3 +126,57 @@ def test_gate_api_functions():
     assert T == ref["threshold"]
     st = E.simulate_gate(lv, T, 3.0, ref["min_hold_frames"])
     assert st == ["C1" if s == 1 else "C2" for s in ref["states"]]
+
+
+@pytest.mark.parametrize("gate_path", ["runscan", "tf"])
+@pytest.mark.parametrize("up_delay_ms", [0.0, 30.0, 250.0])
+def test_gate_paths_multistream(gate_path, up_delay_ms, monkeypatch):
+    """Both gate implementations (closed-form run scan, transfer-function scan)
+    against the reference automaton over the GPU's own frame r, on 3 streams of
+    different lengths whose level toggles around the thresholds every few frames."""
+    torch, E = _engine()
+    from oracle import tomatis_oracle as orc
+    if gate_path == "tf":
+        monkeypatch.setenv("TOMATIS_GATE_TF", "1")
+    else:
+        monkeypatch.delenv("TOMATIS_GATE_TF", raising=False)
+    sr, rng = 44100, np.random.default_rng(int(up_delay_ms) + 7)
+    xs = []
+    for n in (sr * 20 + 77, sr * 9, sr * 31 + 1000):
+        steps = np.repeat(10 ** (rng.uniform(-75, -5, n // 700 + 1) / 20), 700)[:n]
+        xs.append((rng.standard_normal((n, 2)) * steps[:, None]).astype(np.float32))
+    ss = E.StreamSet.from_arrays(xs, sr)
+    pipe = E.GatePipeline(ss, gate_ui=50, n_fft=2048, hop=512, up_delay_ms=up_delay_ms)
+    res = pipe.run()
+    torch.cuda.synchronize()
+    for i in range(3):
+        r = res.stream_r(i)
+        starts = res.first_start[i] + 512 * np.arange(len(r), dtype=np.int64)
+        ref = orc.gate_standard(orc.r_to_level(r), starts, pipe.Ton, pipe.Toff,
+                                pipe.up_delay_samples)
+        st = res.stream_states(i)
+        assert 0 < np.count_nonzero(st == 2) < len(st)
+        np.testing.assert_array_equal(st, ref)
+
+
+def test_fused_limiter_matches_two_pass(monkeypatch):
+    """tomatis_stft_ola_limited (limiter inside the transform kernel) is bit-identical
+    to tomatis_stft_ola + tomatis_apply_limiter on 4 streams with many chunks, loud
+    enough that most chunks are limited."""
+    torch, E = _engine()
+    sr = 48000
+    rng = np.random.default_rng(11)
+    xs = [(rng.standard_normal((n, 2)) * 0.3).astype(np.float32)
+          for n in (sr * 40 + 5, sr * 13, sr * 27 + 999, sr * 6)]
+    outs = []
+    for fuse in ("0", "1"):
+        monkeypatch.setenv("TOMATIS_FUSE_LIMITER", fuse)
+        ss = E.StreamSet.from_arrays(xs, sr)
+        pipe = E.GatePipeline(ss, gate_ui=50, n_fft=2048, hop=512)
+        res = pipe.run()
+        torch.cuda.synchronize()
+        pipe.plan.check_device()
+        outs.append((res.y.cpu().numpy().copy(), res.chunk_peaks.cpu().numpy().copy()))
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+    assert np.count_nonzero(outs[0][1].view(np.float32) > 0.999) > 10
+    np.testing.assert_array_equal(outs[0][0].view(np.uint32), outs[1][0].view(np.uint32))

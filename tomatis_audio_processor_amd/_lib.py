@@ -14,6 +14,7 @@ import ctypes as C
 import os
 
 LIB_NAME = "libtomatis_hip.so"
+ABI_VERSION = 2  # include/tomatis_hip.h TOMATIS_ABI_VERSION
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 F32, F64 = 0, 1
@@ -66,6 +67,8 @@ _SIGS = {
                                          _P, _P]),
     "tomatis_stft_ola": (C.c_int, [_P, _P, _P, C.c_int32, _P, _P, _P, _P]),
     "tomatis_apply_limiter": (C.c_int, [_P, _P, _P, C.c_float, _P]),
+    "tomatis_stft_ola_limited": (C.c_int, [_P, _P, _P, C.c_int32, _P, _P, _P, C.c_float, _P]),
+    "tomatis_plan_error": (C.c_int, [_P, _P]),
     "tomatis_absmax": (C.c_int, [_P, C.c_int64, _P, _P]),
     "tomatis_scale_copy": (C.c_int, [_P, _P, C.c_int64, C.c_float, _P]),
     "tomatis_synth_fill": (C.c_int, [_P, C.c_int64, C.c_int32, C.c_int32, C.c_uint32,
@@ -102,7 +105,7 @@ def lib():
         fn = getattr(h, name)
         fn.restype = res
         fn.argtypes = args
-    if h.tomatis_abi_version() != 1:
+    if h.tomatis_abi_version() != ABI_VERSION:
         raise TomatisLibraryError("ABI version mismatch")
     _LIB = h
     return h

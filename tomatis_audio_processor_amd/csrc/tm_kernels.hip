@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -351,6 +352,152 @@ __global__ __launch_bounds__(256) void k_gate_resolve(const float* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Run-scan gate: the same automaton in closed form when no r can be both "on"
+// and "off" (host-checked from the bit thresholds + exception lists).
+//   A(k) = last frame <= k that is not "on"   (the pending run restarts there)
+//   entry at k  <=>  on(k) and k - A(k) >= D + 1   (pending matured: s_k >= pending)
+//   E(k) = last entry <= k,  F(k) = last "off" frame <= k
+//   state(k) = C2  <=>  E(k) > F(k)
+// Segment summaries compose associatively, so a segment is reduced and scanned
+// in parallel (wave shuffles + LDS), segments are scanned per stream, and every
+// frame resolves from its segment's carry-in.  Frame indices are stream-local.
+// ---------------------------------------------------------------------------
+constexpr int kNI = INT_MIN / 4;  // "none"
+struct GSum {
+  int all_on;  // every frame on
+  int not_on;  // last not-on frame
+  int l_end;   // last frame of the leading on-run (kNI if the first frame is not on)
+  int e_int;   // last entry after the first not-on frame
+  int off;     // last off frame
+};
+struct GCarry {
+  int a, e, f;
+};
+__device__ __forceinline__ GSum gs_identity() { return GSum{1, kNI, kNI, kNI, kNI}; }
+__device__ __forceinline__ GSum gs_frame(int k, uint8_t pr) {
+  if (pr & 1) return GSum{1, kNI, k, kNI, kNI};
+  return GSum{0, k, kNI, kNI, (pr & 2) ? k : kNI};
+}
+__device__ __forceinline__ GSum gs_cat(const GSum& X, const GSum& Y, int D) {
+  GSum Z;
+  Z.all_on = X.all_on & Y.all_on;
+  Z.not_on = max(X.not_on, Y.not_on);
+  Z.off = max(X.off, Y.off);
+  if (X.all_on) {
+    Z.l_end = (Y.l_end != kNI) ? Y.l_end : X.l_end;
+    Z.e_int = Y.e_int;
+  } else {
+    Z.l_end = X.l_end;
+    const int lead = (Y.l_end != kNI && Y.l_end >= X.not_on + D + 1) ? Y.l_end : kNI;
+    Z.e_int = max(max(X.e_int, Y.e_int), lead);
+  }
+  return Z;
+}
+__device__ __forceinline__ GCarry gs_apply(const GCarry& c, const GSum& S, int D) {
+  GCarry o;
+  o.a = S.all_on ? c.a : S.not_on;
+  const int lead = (S.l_end != kNI && S.l_end >= c.a + D + 1) ? S.l_end : kNI;
+  o.e = max(max(c.e, S.e_int), lead);
+  o.f = max(c.f, S.off);
+  return o;
+}
+__device__ __forceinline__ GSum gs_shfl_up(const GSum& x, int d) {
+  return GSum{__shfl_up(x.all_on, d, 64), __shfl_up(x.not_on, d, 64), __shfl_up(x.l_end, d, 64),
+              __shfl_up(x.e_int, d, 64), __shfl_up(x.off, d, 64)};
+}
+// inclusive scan over the 256 threads of a block (thread order); returns the
+// thread's EXCLUSIVE prefix and sets tot to the block total
+__device__ GSum gs_block_scan(GSum v, int D, GSum& tot) {
+  __shared__ GSum s_w[4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  GSum inc = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const GSum y = gs_shfl_up(inc, d);
+    if (lane >= d) inc = gs_cat(y, inc, D);
+  }
+  if (lane == 63) s_w[wv] = inc;
+  __syncthreads();
+  GSum wpre = gs_identity();
+  for (int w = 0; w < wv; ++w) wpre = gs_cat(wpre, s_w[w], D);
+  tot = gs_identity();
+  for (int w = 0; w < 4; ++w) tot = gs_cat(tot, s_w[w], D);
+  GSum ex = gs_shfl_up(inc, 1);
+  if (lane == 0) ex = gs_identity();
+  __syncthreads();
+  return gs_cat(wpre, ex, D);
+}
+
+// pass 1: one block per gate segment (<= 1024 frames, 4 per thread) -> summary
+__global__ __launch_bounds__(256) void k_gate_sum(const float* __restrict__ r,
+                                                  const TomatisStream* __restrict__ st,
+                                                  const GateSeg* __restrict__ segs, int D,
+                                                  GSum* __restrict__ sums) {
+  const GateSeg G = segs[blockIdx.x];
+  const TomatisStream S = st[G.s];
+  GSum v = gs_identity();
+  const int i0 = 4 * threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int i = i0 + j;
+    if (i < G.nf) v = gs_cat(v, gs_frame((int)G.k0 + i, gate_pred(r[S.frame_base + G.k0 + i], S)), D);
+  }
+  GSum tot;
+  (void)gs_block_scan(v, D, tot);
+  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+// pass 2: one block per stream, scan of segment summaries -> carry-in per segment
+__global__ __launch_bounds__(256) void k_gate_carry(const int32_t* __restrict__ seg_first,
+                                                    const int32_t* __restrict__ seg_count, int D,
+                                                    const GSum* __restrict__ sums,
+                                                    GCarry* __restrict__ carry) {
+  const int a = seg_first[blockIdx.x], n = seg_count[blockIdx.x];
+  GCarry c{-1, kNI, kNI};  // initial C1 idle: run "restarts" just before frame 0
+  for (int t0 = 0; t0 < n; t0 += 256) {
+    const int i = t0 + threadIdx.x;
+    const GSum v = (i < n) ? sums[a + i] : gs_identity();
+    GSum tot;
+    const GSum ex = gs_block_scan(v, D, tot);
+    if (i < n) carry[a + i] = gs_apply(c, ex, D);
+    c = gs_apply(c, tot, D);
+  }
+}
+
+// pass 3: one block per segment: frame states from the carry-in
+__global__ __launch_bounds__(256) void k_gate_states(const float* __restrict__ r,
+                                                     const TomatisStream* __restrict__ st,
+                                                     const GateSeg* __restrict__ segs, int D,
+                                                     const GCarry* __restrict__ carry,
+                                                     uint8_t* __restrict__ states,
+                                                     uint16_t* __restrict__ rows) {
+  const GateSeg G = segs[blockIdx.x];
+  const TomatisStream S = st[G.s];
+  const int i0 = 4 * threadIdx.x;
+  uint8_t pr[4];
+  GSum v = gs_identity();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int i = i0 + j;
+    pr[j] = (i < G.nf) ? gate_pred(r[S.frame_base + G.k0 + i], S) : 0;
+    if (i < G.nf) v = gs_cat(v, gs_frame((int)G.k0 + i, pr[j]), D);
+  }
+  GSum tot;
+  const GSum ex = gs_block_scan(v, D, tot);
+  GCarry c = gs_apply(carry[blockIdx.x], ex, D);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int i = i0 + j;
+    if (i < G.nf) {
+      c = gs_apply(c, gs_frame((int)G.k0 + i, pr[j]), D);
+      const uint8_t stt = (c.e > c.f) ? 2 : 1;
+      states[S.frame_base + G.k0 + i] = stt;
+      if (rows) rows[S.frame_base + G.k0 + i] = (uint16_t)(stt - 1);
+    }
+  }
+}
+
 // ===========================================================================
 // alpha scans (sequential per stream; f64 exactly as the reference)
 // ===========================================================================
@@ -536,6 +683,13 @@ struct MainArgs {
   cf* scratch;          // generic path: [frames][N]
   int n_runs, hop, n_bins, ch, norm_mode, rmax, n_rows_lds;
   float inv_n;
+  // fused limiter (limit > 0): per-chunk flush counters, flushes expected,
+  // output ranges; every wave rescales its own output once its chunks are final
+  float limit;
+  uint32_t* chunk_done;
+  const uint32_t* chunk_need;
+  const int64_t* chunk_rng;  // [2 * chunk]: output-relative [p0, p1)
+  uint32_t* err;
 };
 
 __device__ __forceinline__ float norm_den(float w, int mode) {
@@ -562,10 +716,65 @@ __device__ __forceinline__ int chunk_of(int64_t p, const TomatisStream& S) {
 
 template <int P>
 __device__ __forceinline__ void flush_peak(float& pk, int cid, const TomatisStream& S,
-                                           uint32_t* peaks, int L) {
+                                           uint32_t* peaks, int L, uint32_t* done) {
   const float m = wave_max(pk);  // P > 64: each wave flushes its partial max
-  if ((L & 63) == 0 && m > 0.f) atomicMax(peaks + S.chunk_base + cid, __float_as_uint(m));
+  if ((L & 63) == 0) {
+    if (m > 0.f) atomicMax(peaks + S.chunk_base + cid, __float_as_uint(m));
+    if (done) {  // fused limiter: the max lands before the flush is counted
+      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(done + S.chunk_base + cid, 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   pk = 0.f;
+}
+
+// fused limiter tail of one wave: wait until every flush of chunk gc has been
+// counted (all contributors are dispatched no later than this wave's
+// neighbours), then scale this wave's own samples of the chunk.
+template <int CH>
+__device__ void limit_own(const MainArgs& A, const TomatisStream& S, int gc, int64_t lo,
+                          int64_t hi, int lane) {
+  const uint32_t need = A.chunk_need[gc];
+  uint32_t got = 0;
+  for (int spin = 0; spin < (1 << 18); ++spin) {
+    got = __hip_atomic_load(A.chunk_done + gc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    got = __builtin_amdgcn_readfirstlane(got);
+    if (got >= need) break;
+    __builtin_amdgcn_s_sleep(32);
+  }
+  if (got < need) {  // never expected; leaves the chunk unscaled and reports it
+    if (lane == 0) atomicOr(A.err, 1u);
+    return;
+  }
+  const float peak = __uint_as_float(__builtin_amdgcn_readfirstlane(
+      __hip_atomic_load(A.peaks + gc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+  if (!(peak > A.limit)) return;
+  const float sc = A.limit / peak;
+  const int64_t a = max(lo, A.chunk_rng[2 * gc]), b = min(hi, A.chunk_rng[2 * gc + 1]);
+  if (b <= a) return;
+  float* base = A.y + S.out_off + a * CH;
+  int64_t n = (b - a) * CH;
+  // scalar head up to 16-byte alignment, float4 body (16 in flight per lane), tail
+  const int head = (int)min<int64_t>(n, (4 - (int)((reinterpret_cast<uintptr_t>(base) >> 2) & 3)) & 3);
+  if (lane < head) base[lane] = base[lane] * sc;
+  base += head;
+  n -= head;
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  f4v* b4 = reinterpret_cast<f4v*>(base);
+  const int64_t n4 = n >> 2;
+  constexpr int U = 16;
+  for (int64_t i = lane; i < n4; i += 64 * U) {
+    f4v t[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i + 64 * u < n4) t[u] = __builtin_nontemporal_load(b4 + i + 64 * u);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i + 64 * u < n4) __builtin_nontemporal_store(t[u] * sc, b4 + i + 64 * u);
+  }
+  const int64_t t0 = n4 << 2;
+  if (t0 + lane < n) base[t0 + lane] = base[t0 + lane] * sc;
 }
 
 template <int CH>
@@ -677,6 +886,8 @@ __global__ __launch_bounds__(256, 2) void k_stft_ola(MainArgs A) {
   // chunk tracking by frame index (host guarantees hop-aligned chunk boundaries)
   const int64_t s_ka = S.first_start + R.ka * HOP;
   int cid = chunk_of(s_ka, S);
+  const int cid_first = cid;
+  uint32_t* const done = (A.limit > 0.f) ? A.chunk_done : nullptr;
   int64_t next_chunk_k = INT64_MAX;
   if (S.n_chunks > 1 && cid < S.n_chunks - 1)
     next_chunk_k = (S.chunk_first + (int64_t)cid * S.chunk_len - S.first_start) / HOP;
@@ -749,7 +960,7 @@ __global__ __launch_bounds__(256, 2) void k_stft_ola(MainArgs A) {
     for (int i = NC; i < NR; ++i) v[i] = cscale(v[i], s_win[L + P * i]);
     if (live && k >= R.ka) {
       if (k == next_chunk_k) {
-        flush_peak<P>(pk, cid, S, A.peaks, L);
+        flush_peak<P>(pk, cid, S, A.peaks, L, done);
         ++cid;
         next_chunk_k = (cid < S.n_chunks - 1) ? next_chunk_k + chunk_k_step : INT64_MAX;
       }
@@ -793,7 +1004,19 @@ __global__ __launch_bounds__(256, 2) void k_stft_ola(MainArgs A) {
 #pragma unroll
     for (int i = 0; i < NC; ++i) acc[i] = v[i + SH];
   }
-  if (valid) flush_peak<P>(pk, cid, S, A.peaks, L);
+  if (valid) flush_peak<P>(pk, cid, S, A.peaks, L, done);
+  if (valid && done) {
+    // this wave's own output range (stores of frames [ka, kb) and the stream tail)
+    const int64_t s_last = S.first_start + (R.kb - 1) * HOP;
+    const int64_t lo = max(s_ka, S.out_begin) - S.out_begin;
+    const int64_t hi = min(s_last + (R.last ? (int64_t)N : (int64_t)HOP), out_end) - S.out_begin;
+    // P > 64: both waves of the sequence cover the same range; split it by wave
+    const int nw = P / 64, w = L >> 6;
+    const int64_t span = hi - lo, per = (span + nw - 1) / nw;
+    const int64_t wlo = lo + per * w, whi = min(hi, wlo + per);
+    for (int c = cid_first; c <= cid; ++c)
+      limit_own<CH>(A, S, S.chunk_base + c, wlo, whi, L & 63);
+  }
 }
 
 // Generic hop: same transform, windowed frame outputs to scratch, then a gather.
@@ -1040,6 +1263,16 @@ struct tomatis_plan_s {
   int64_t* mh_off = nullptr;
   float* gperm = nullptr;
   int gperm_rows = 0;
+  // fused limiter
+  uint32_t* chunk_need = nullptr;
+  uint32_t* chunk_done = nullptr;
+  int64_t* chunk_rng = nullptr;
+  uint32_t* err = nullptr;
+  int fuse_span = 0;  // max runs contributing to one chunk
+  // run-scan gate (exclusive on/off predicates)
+  bool gate_excl = false;
+  void* gsum = nullptr;
+  void* gcarry = nullptr;
   // streaming levels (hop % 128 == 0): per-stream 8-block groups and leaves
   bool leaf_path = false;
   int64_t n_groups = 0;
@@ -1115,7 +1348,8 @@ int tomatis_plan_destroy(tomatis_plan_t p) {
   void* ptrs[] = {p->st, p->runs, p->lblocks, p->segs, p->seg_first, p->seg_count, p->tf,
                   p->seg_start, p->win, p->win2, p->winv, p->twN, p->twP, p->scratch,
                   p->pos_base, p->chunks, p->mh_tf, p->mh_cnt, p->mh_off, p->gperm,
-                  p->grp_base, p->leaf_base, p->leaves};
+                  p->grp_base, p->leaf_base, p->leaves, p->gsum, p->gcarry,
+                  p->chunk_need, p->chunk_done, p->chunk_rng, p->err};
   for (void* q : ptrs) dfree(q);
   delete p;
   return TOMATIS_OK;
@@ -1123,6 +1357,24 @@ int tomatis_plan_destroy(tomatis_plan_t p) {
 
 int64_t tomatis_plan_total_frames(tomatis_plan_t p) { return p ? p->total_frames : -1; }
 int32_t tomatis_plan_total_chunks(tomatis_plan_t p) { return p ? p->total_chunks : -1; }
+
+// no float32 bit pattern can satisfy both gate predicates (run-scan gate valid)
+static bool gate_exclusive(const TomatisStream& S) {
+  auto in = [](uint32_t b, const uint32_t* e, int n) {
+    for (int i = 0; i < n; ++i)
+      if (e[i] == b) return true;
+    return false;
+  };
+  auto on = [&](uint32_t b) { return (b >= S.on_bits) != in(b, S.on_exc, S.n_on_exc); };
+  auto off = [&](uint32_t b) { return (b <= S.off_bits) != in(b, S.off_exc, S.n_off_exc); };
+  if (S.n_on_exc < 0 || S.n_on_exc > 4 || S.n_off_exc < 0 || S.n_off_exc > 4) return false;
+  if (S.on_bits <= S.off_bits) return false;
+  for (int i = 0; i < S.n_on_exc; ++i)
+    if (on(S.on_exc[i]) && off(S.on_exc[i])) return false;
+  for (int i = 0; i < S.n_off_exc; ++i)
+    if (on(S.off_exc[i]) && off(S.off_exc[i])) return false;
+  return true;
+}
 
 static int plan_build(tomatis_plan_s* p, const float* window) {
   const TomatisPlanDesc& d = p->d;
@@ -1208,6 +1460,12 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
     }
     p->n_segs = (int)sg.size();
     if ((rc = dalloc_copy(&p->segs, sg))) return rc;
+    p->gate_excl = env_int("TOMATIS_GATE_TF", 0) == 0;
+    for (int s = 0; s < ns; ++s) p->gate_excl = p->gate_excl && gate_exclusive(p->hs[s]);
+    if (p->n_segs > 0) {
+      if (hipMalloc(&p->gsum, (size_t)p->n_segs * 5 * sizeof(int))) return TOMATIS_E_NOMEM;
+      if (hipMalloc(&p->gcarry, (size_t)p->n_segs * 3 * sizeof(int))) return TOMATIS_E_NOMEM;
+    }
     if ((rc = dalloc_copy(&p->seg_first, first))) return rc;
     if ((rc = dalloc_copy(&p->seg_count, count))) return rc;
     const int nstate = d.up_delay_frames + 2;
@@ -1279,6 +1537,56 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
     p->total_out = tot;
     if ((rc = dalloc_copy(&p->chunks, cd))) return rc;
     if ((rc = dalloc_copy(&p->pos_base, pb))) return rc;
+    // fused limiter: flushes expected per chunk (host mirror of the kernel's
+    // frame-indexed chunk walk), chunk output ranges, eligibility
+    if (!p->generic && p->total_chunks > 0) {
+      const int HOP = hop, wpr = P / 64;
+      std::vector<uint32_t> need(p->total_chunks, 0);
+      std::vector<int64_t> rng(2 * (size_t)p->total_chunks, 0);
+      for (const ChunkDesc& C : cd) {
+        rng[2 * (p->hs[C.s].chunk_base + C.c)] = C.p0;
+        rng[2 * (p->hs[C.s].chunk_base + C.c) + 1] = C.p1;
+      }
+      std::vector<int32_t> first_run(p->total_chunks, -1), last_run(p->total_chunks, -1);
+      for (int ri = 0; ri < (int)runs.size(); ++ri) {
+        const Run& R = runs[ri];
+        const TomatisStream& S = p->hs[R.s];
+        const int64_t s_ka = S.first_start + R.ka * HOP;
+        int cid = 0;
+        if (S.n_chunks > 1 && s_ka >= S.chunk_first)
+          cid = (int)std::min<int64_t>(1 + (s_ka - S.chunk_first) / S.chunk_len, S.n_chunks - 1);
+        int64_t next_k = INT64_MAX;
+        if (S.n_chunks > 1 && cid < S.n_chunks - 1)
+          next_k = (S.chunk_first + (int64_t)cid * S.chunk_len - S.first_start) / HOP;
+        const int64_t step = S.n_chunks > 1 ? S.chunk_len / HOP : 0;
+        auto mark = [&](int c) {
+          const int g = S.chunk_base + c;
+          need[g] += wpr;
+          if (first_run[g] < 0) first_run[g] = ri;
+          last_run[g] = ri;
+        };
+        while (next_k < R.kb) {
+          if (next_k >= R.ka) {
+            mark(cid);
+            ++cid;
+            next_k = (cid < S.n_chunks - 1) ? next_k + step : INT64_MAX;
+          } else {
+            break;  // cannot happen: next chunk starts after the run's first frame
+          }
+        }
+        mark(cid);
+      }
+      int span = 0;
+      for (int g = 0; g < p->total_chunks; ++g)
+        if (first_run[g] >= 0) span = std::max(span, last_run[g] - first_run[g] + 1);
+      p->fuse_span = span;
+      if ((rc = dalloc_copy(&p->chunk_need, need))) return rc;
+      if ((rc = dalloc_copy(&p->chunk_rng, rng))) return rc;
+      if (hipMalloc(reinterpret_cast<void**>(&p->chunk_done), (size_t)p->total_chunks * 4))
+        return TOMATIS_E_NOMEM;
+    }
+    if (hipMalloc(reinterpret_cast<void**>(&p->err), 4)) return TOMATIS_E_NOMEM;
+    if (hipMemset(p->err, 0, 4)) return TOMATIS_E_HIP;
   }
   // --- generic-hop scratch ---
   if (p->generic && p->total_frames > 0) {
@@ -1363,12 +1671,23 @@ int tomatis_plan_create(tomatis_plan_t* out, const TomatisPlanDesc* desc, const 
 
 int tomatis_plan_update_streams(tomatis_plan_t p, const TomatisStream* streams, void* hs) {
   if (!p || !streams) return TOMATIS_E_ARG;
+  for (int i = 0; i < p->n_streams; ++i) {  // geometry is fixed at plan creation
+    const TomatisStream &a = streams[i], &b = p->hs[i];
+    if (a.in_off != b.in_off || a.out_off != b.out_off || a.n != b.n ||
+        a.first_start != b.first_start || a.n_frames != b.n_frames ||
+        a.out_begin != b.out_begin || a.out_len != b.out_len || a.chunk_first != b.chunk_first ||
+        a.chunk_len != b.chunk_len || a.n_chunks != b.n_chunks)
+      return TOMATIS_E_ARG;
+  }
+  bool excl = env_int("TOMATIS_GATE_TF", 0) == 0;
   for (int i = 0; i < p->n_streams; ++i) {
     TomatisStream s = streams[i];
     s.frame_base = p->hs[i].frame_base;
     s.chunk_base = p->hs[i].chunk_base;
     p->hs[i] = s;
+    excl = excl && gate_exclusive(s);
   }
+  p->gate_excl = excl;
   if (p->n_streams == 0) return TOMATIS_OK;
   return hipfail(hipMemcpyAsync(p->st, p->hs.data(), p->hs.size() * sizeof(TomatisStream),
                                 hipMemcpyHostToDevice, (hipStream_t)hs));
@@ -1450,13 +1769,22 @@ int tomatis_gate_std(tomatis_plan_t p, const float* r, uint8_t* states, uint16_t
   if (p->n_segs == 0) return TOMATIS_OK;
   hipStream_t s = (hipStream_t)hs;
   const int D = p->d.up_delay_frames;
-  hipLaunchKernelGGL(k_gate_tf, dim3((p->n_segs + 3) / 4), dim3(256), 0, s, r, p->st, p->segs,
-                     p->n_segs, D, p->tf);
-  hipLaunchKernelGGL(k_gate_chain, dim3((p->n_streams + 63) / 64), dim3(64), 0, s, p->st,
-                     p->n_streams, p->seg_first, p->seg_count, D + 2, p->tf, p->seg_start, 0);
   const bool xf = p->d.alpha_mode == 1;
-  hipLaunchKernelGGL(k_gate_resolve, dim3((p->n_segs + 3) / 4), dim3(256), 0, s, r, p->st,
-                     p->segs, p->n_segs, D, p->seg_start, states, xf ? nullptr : rows);
+  if (p->gate_excl) {
+    hipLaunchKernelGGL(k_gate_sum, dim3(p->n_segs), dim3(256), 0, s, r, p->st, p->segs, D,
+                       (GSum*)p->gsum);
+    hipLaunchKernelGGL(k_gate_carry, dim3(p->n_streams), dim3(256), 0, s, p->seg_first,
+                       p->seg_count, D, (const GSum*)p->gsum, (GCarry*)p->gcarry);
+    hipLaunchKernelGGL(k_gate_states, dim3(p->n_segs), dim3(256), 0, s, r, p->st, p->segs, D,
+                       (const GCarry*)p->gcarry, states, xf ? nullptr : rows);
+  } else {
+    hipLaunchKernelGGL(k_gate_tf, dim3((p->n_segs + 3) / 4), dim3(256), 0, s, r, p->st, p->segs,
+                       p->n_segs, D, p->tf);
+    hipLaunchKernelGGL(k_gate_chain, dim3((p->n_streams + 63) / 64), dim3(64), 0, s, p->st,
+                       p->n_streams, p->seg_first, p->seg_count, D + 2, p->tf, p->seg_start, 0);
+    hipLaunchKernelGGL(k_gate_resolve, dim3((p->n_segs + 3) / 4), dim3(256), 0, s, r, p->st,
+                       p->segs, p->n_segs, D, p->seg_start, states, xf ? nullptr : rows);
+  }
   if (xf) {
     hipLaunchKernelGGL(k_alpha_xfade, dim3((p->n_streams + 63) / 64), dim3(64), 0, s, p->st,
                        p->n_streams, states, p->d.xfade_frames, rows, alpha_out);
@@ -1476,8 +1804,9 @@ int tomatis_minhold_bisect(tomatis_plan_t p, const double* levels, const double*
   return launch_check();
 }
 
-int tomatis_stft_ola(tomatis_plan_t p, const float* x, const float* gains, int32_t n_rows,
-                     const uint16_t* rows, float* y, uint32_t* peaks, void* hs) {
+static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, int32_t n_rows,
+                         const uint16_t* rows, float* y, uint32_t* peaks, float limit,
+                         void* hs) {
   if (!p || !x || !gains || !rows || !y || !peaks || n_rows < 1) return TOMATIS_E_ARG;
   if (p->n_runs == 0) return TOMATIS_OK;
   hipStream_t s = (hipStream_t)hs;
@@ -1518,6 +1847,15 @@ int tomatis_stft_ola(tomatis_plan_t p, const float* x, const float* gains, int32
   A.rmax = p->generic ? 1 : p->rmax;
   A.inv_n = 1.0f / (float)N;
   A.n_rows_lds = (n_rows <= 2 && N <= 2048) ? n_rows : 0;
+  A.limit = limit;
+  A.chunk_done = p->chunk_done;
+  A.chunk_need = p->chunk_need;
+  A.chunk_rng = p->chunk_rng;
+  A.err = p->err;
+  if (limit > 0.f) {
+    if (!p->chunk_done) return TOMATIS_E_UNSUPPORTED;
+    if (hipMemsetAsync(p->chunk_done, 0, (size_t)p->total_chunks * 4, s)) return TOMATIS_E_HIP;
+  }
   const int nseq = 256 / p->P;
   const int blocks = (p->n_runs + nseq - 1) / nseq;
   const int ch = p->d.ch;
@@ -1546,6 +1884,35 @@ int tomatis_stft_ola(tomatis_plan_t p, const float* x, const float* gains, int32
     else launch_main<128, 32, 16>(A, ch, blocks, s);
   }
   return launch_check();
+}
+
+int tomatis_stft_ola(tomatis_plan_t p, const float* x, const float* gains, int32_t n_rows,
+                     const uint16_t* rows, float* y, uint32_t* peaks, void* hs) {
+  return stft_ola_impl(p, x, gains, n_rows, rows, y, peaks, 0.f, hs);
+}
+
+// chunks whose flushes come from at most this many consecutive runs are limited
+// inside the main kernel (waves wait only on near neighbours)
+constexpr int kFuseMaxSpan = 64;
+
+int tomatis_stft_ola_limited(tomatis_plan_t p, const float* x, const float* gains,
+                             int32_t n_rows, const uint16_t* rows, float* y, uint32_t* peaks,
+                             float limit, void* hs) {
+  if (!p || !(limit > 0.f)) return TOMATIS_E_ARG;
+  const bool fuse = !p->generic && p->chunk_done && p->fuse_span > 0 &&
+                    p->fuse_span <= kFuseMaxSpan && env_int("TOMATIS_FUSE_LIMITER", 1) != 0;
+  if (fuse) return stft_ola_impl(p, x, gains, n_rows, rows, y, peaks, limit, hs);
+  int rc = stft_ola_impl(p, x, gains, n_rows, rows, y, peaks, 0.f, hs);
+  if (rc) return rc;
+  return tomatis_apply_limiter(p, y, peaks, limit, hs);
+}
+
+int tomatis_plan_error(tomatis_plan_t p, void* hs) {
+  if (!p || !p->err) return TOMATIS_E_ARG;
+  uint32_t e = 0;
+  if (hipMemcpyAsync(&e, p->err, 4, hipMemcpyDeviceToHost, (hipStream_t)hs)) return TOMATIS_E_HIP;
+  if (hipStreamSynchronize((hipStream_t)hs)) return TOMATIS_E_HIP;
+  return e ? TOMATIS_E_HIP : TOMATIS_OK;
 }
 
 int tomatis_apply_limiter(tomatis_plan_t p, float* y, const uint32_t* peaks, float limit, void* hs) {

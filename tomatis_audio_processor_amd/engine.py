@@ -104,6 +104,10 @@ class Plan:
         check(self.L.tomatis_plan_update_streams(self.h, self.streams, stream_handle()),
               "plan_update_streams")
 
+    def check_device(self):
+        """Raise if a device-side consistency check fired (synchronises)."""
+        check(self.L.tomatis_plan_error(self.h, stream_handle()), "plan_error")
+
     def close(self):
         if getattr(self, "h", None):
             self.L.tomatis_plan_destroy(self.h)
@@ -274,12 +278,12 @@ class GatePipeline:
                                  ptr(self.alpha), hs), "gate_std")
         if marks:
             marks[0].record()
-        check(L.tomatis_stft_ola(P, ptr(self.ss.x), ptr(self.gains), self.n_rows,
-                                 ptr(self.rows), ptr(self.y), ptr(self.peaks), hs), "stft_ola")
+        # transform + OLA + per-chunk limiter (fused in-kernel when chunks are short)
+        check(L.tomatis_stft_ola_limited(P, ptr(self.ss.x), ptr(self.gains), self.n_rows,
+                                         ptr(self.rows), ptr(self.y), ptr(self.peaks),
+                                         PEAK_LIMIT, hs), "stft_ola_limited")
         if marks:
             marks[1].record()
-        check(L.tomatis_apply_limiter(P, ptr(self.y), ptr(self.peaks), PEAK_LIMIT, hs),
-              "apply_limiter")
         return self.result()
 
     def result(self) -> Result:
