@@ -1,4 +1,14 @@
-"""Build ``libtomatis_hip.so`` in-tree with hipcc for gfx950 (no cmake/ninja needed)."""
+"""Build ``libtomatis_hip.so`` in-tree with hipcc for gfx950 (no cmake/ninja needed).
+
+Two translation units, compiled in parallel and linked into one C-ABI library:
+
+* ``tm_kernels.hip``   levels, gate, limiter, plan and the ``extern "C"`` entry points;
+* ``tm_transform.hip`` the fused transform kernels, compiled with the max-ILP
+  machine scheduler (``-amdgpu-sched-strategy=max-ilp``), which keeps the
+  per-frame LDS table reads batched instead of serialising them.  The other unit
+  keeps the default scheduler so the streaming kernels stay at low register
+  counts (high occupancy).
+"""
 from __future__ import annotations
 
 import os
@@ -7,12 +17,17 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRC = os.path.join(HERE, "csrc", "tm_kernels.hip")
-DEPS = [SRC, os.path.join(HERE, "csrc", "tm_common.h"), os.path.join(HERE, "csrc", "tm_fft.h"),
-        os.path.join(ROOT, "include", "tomatis_hip.h")]
+CSRC = os.path.join(HERE, "csrc")
+UNITS = {  # source -> extra flags
+    "tm_kernels.hip": [],
+    "tm_transform.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+}
+DEPS = [os.path.join(CSRC, f) for f in (*UNITS, "tm_common.h", "tm_fft.h", "tm_shared.h")] + \
+       [os.path.join(ROOT, "include", "tomatis_hip.h")]
 OUT = os.path.join(HERE, "libtomatis_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "-fPIC", "-shared",
+ARCH = "--offload-arch=gfx950"
+FLAGS = [ARCH, "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "-fPIC",
          "-I" + os.path.join(ROOT, "include")]
 
 
@@ -23,16 +38,34 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in DEPS)
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
-    if not force and not needs_build():
+def build(force: bool = False, verbose: bool = True, out: str = OUT, extra=()) -> str:
+    """Compile the C-ABI library; ``out``/``extra`` build experiment variants."""
+    if out == OUT and not extra and not force and not needs_build():
         return OUT
-    cmd = [HIPCC, *FLAGS, "-o", OUT + ".tmp", SRC]
+    objs, procs = [], []
+    for src, fl in UNITS.items():
+        obj = f"{out}.{src}.o"
+        cmd = [HIPCC, *FLAGS, *fl, *extra, "-c", "-o", obj, os.path.join(CSRC, src)]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        procs.append(subprocess.Popen(cmd))
+        objs.append(obj)
+    rcs = [p.wait() for p in procs]
+    if any(rcs):
+        raise subprocess.CalledProcessError(max(rcs), "hipcc")
+    link = [HIPCC, ARCH, "-shared", "-fPIC", "-o", out + ".tmp", *objs]
     if verbose:
-        print(" ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+        print(" ".join(link), flush=True)
+    subprocess.run(link, check=True)
+    os.replace(out + ".tmp", out)
+    for o in objs:
+        os.remove(o)
+    return out
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    # python -m tomatis_audio_processor_amd.build [--force] [--out PATH -- extra hipcc flags]
+    a = sys.argv[1:]
+    extra = a[a.index("--") + 1:] if "--" in a else []
+    out = a[a.index("--out") + 1] if "--out" in a else OUT
+    build(force="--force" in a, out=out, extra=extra)

@@ -48,7 +48,8 @@ __device__ __forceinline__ void xsync() {
 __device__ __forceinline__ int x2col(int a, int c) { return 8 * c + (a ^ (c & 7)); }
 
 // forward FFT.  v: 32 registers (input x[L + P*n2]); out: bin layout above.
-// twN: LDS [32][P] with W_N^{n1*k2}; twP: LDS [P] with W_P^m; buf: round buffer.
+// twN: LDS W_N^{n1*k2} in lane-pair layout [k2/2][n1][k2&1] (16-B aligned);
+// twP: LDS [P] with W_P^m; buf: round buffer.
 template <int P, int NR = 32>
 __device__ __forceinline__ void fft_fwd(cf (&v)[NR], int L, const cf* twN, const cf* twP,
                                         cf* buf) {
@@ -58,10 +59,12 @@ __device__ __forceinline__ void fft_fwd(cf (&v)[NR], int L, const cf* twN, const
   const int c3 = L % PB, q3 = L / PB;
   // step 1
   dft<NR, false, 0, 1, NR>(v);
-  // step 2
-  sfor<1, NR>([&](auto kk) {
-    constexpr int K = decltype(kk)::value;
-    v[K] = cmul(v[K], twN[K * P + L]);
+  // step 2 (twiddles in lane-pair layout: one ds_read_b128 per two registers)
+  sfor<0, NR / 2>([&](auto kk) {
+    constexpr int K2 = decltype(kk)::value;
+    const float4 t = reinterpret_cast<const float4*>(twN)[K2 * P + L];
+    if constexpr (K2 > 0) v[2 * K2] = cmul(v[2 * K2], cf{t.x, t.y});
+    v[2 * K2 + 1] = cmul(v[2 * K2 + 1], cf{t.z, t.w});
   });
   // exchange 1 : (lane n1, reg k2) -> (lane (a,q), reg (j,b))
   sfor<0, G::ROUNDS>([&](auto rr) {
@@ -176,12 +179,21 @@ __device__ __forceinline__ void fft_inv(cf (&v)[NR], int L, const cf* twN, const
     xsync<P>();
   });
   // step 2': conj W_N^{n1 k2}
-  sfor<1, NR>([&](auto kk) {
-    constexpr int K = decltype(kk)::value;
-    v[K] = cmulc(v[K], twN[K * P + L]);
+  sfor<0, NR / 2>([&](auto kk) {
+    constexpr int K2 = decltype(kk)::value;
+    const float4 t = reinterpret_cast<const float4*>(twN)[K2 * P + L];
+    if constexpr (K2 > 0) v[2 * K2] = cmulc(v[2 * K2], cf{t.x, t.y});
+    v[2 * K2 + 1] = cmulc(v[2 * K2 + 1], cf{t.z, t.w});
   });
   // step 1': IDFT_NR over k2 -> n2
   dft<NR, true, 0, 1, NR>(v);
+}
+
+// per-lane register tables (window, gains, 1/wsum) in lane-quad layout:
+// element (register i, lane L) at ((i/4)*P + L)*4 + i%4, read with ds_read_b128
+template <int P>
+__device__ __forceinline__ constexpr int lq(int i, int L) {
+  return ((i >> 2) * P + L) * 4 + (i & 3);
 }
 
 // bin index held by lane L, register index i (= j'*8 + d) after fft_fwd

@@ -1,0 +1,62 @@
+// tm_shared.h — types shared by the two translation units of libtomatis_hip:
+// tm_kernels.hip (levels, gate, limiter, plan, C ABI) and tm_transform.hip
+// (the fused transform kernels, compiled with the max-ILP scheduler).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tm_common.h"
+#include "../../include/tomatis_hip.h"
+
+namespace tshared {
+using tdsp::cf;
+
+constexpr float kEps32 = 1e-12f;  // EPS as the reference adds it to float32 arrays
+constexpr double kEps64 = 1e-12;
+
+struct Run {          // main-kernel work item: emit frames [ka, kb) of stream s
+  int32_t s;
+  int32_t last;       // 1 if kb is the stream's last frame + 1
+  int64_t ka, kb;
+};
+
+__device__ __forceinline__ int64_t floordiv(int64_t a, int64_t b) {
+  int64_t q = a / b;
+  return (q * b > a) ? q - 1 : q;
+}
+
+struct MainArgs {
+  const float* x;
+  float* y;
+  const float* gains;   // [rows][N] gain per (lane, register) in bin layout (see gain_perm)
+  const uint16_t* rows;
+  uint32_t* peaks;
+  const TomatisStream* st;
+  const Run* runs;
+  const float* win;     // [N]
+  const float* win2;    // [N] win*win (f32)
+  const cf* twN;        // [32][P]
+  const cf* twP;        // [P]
+  const float* winv;    // [hop] 1/(interior wsum) (already normalisation-rule applied)
+  cf* scratch;          // generic path: [frames][N]
+  int n_runs, hop, n_bins, ch, norm_mode, rmax, n_rows_lds;
+  float inv_n;
+  // fused limiter (limit > 0): per-chunk flush counters, flushes expected,
+  // output ranges; every wave rescales its own output once its chunks are final
+  float limit;
+  uint32_t* chunk_done;
+  const uint32_t* chunk_need;
+  const int64_t* chunk_rng;  // [2 * chunk]: output-relative [p0, p1)
+  uint32_t* err;
+};
+
+// launchers (tm_transform.hip); kernels stay private to that unit
+void launch_transform(const MainArgs& A, int P, int NR, int SH, int ch, int blocks, hipStream_t s);
+void launch_frames(const MainArgs& A, int P, int NR, int blocks, hipStream_t s);
+void launch_gain_perm(int P, int NR, const float* gains, int n_rows, int n_bins, float* out,
+                      hipStream_t s);
+void launch_ola_gather(const MainArgs& A, int n_streams, const int64_t* pos_base, int64_t total,
+                       int N, hipStream_t s);
+int env_int(const char* name, int dflt);
+
+}  // namespace tshared

@@ -1,0 +1,584 @@
+// tm_transform.hip — the fused framing -> window -> FFT -> gain -> IFFT ->
+// window -> OLA -> normalise (-> limiter) kernels for gfx950, and their
+// launchers.  Own translation unit: built with the max-ILP machine scheduler,
+// which batches the per-frame LDS table reads instead of serialising them.
+// Reference: src/process_tomatis.py:394-406,419-426,451-453 (see tm_kernels.hip).
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdint>
+
+#include "tm_common.h"
+#include "tm_fft.h"
+#include "tm_shared.h"
+
+using namespace tdsp;
+using namespace tshared;
+
+namespace {
+// ===========================================================================
+// Fused STFT -> gain -> ISTFT -> OLA -> normalise (register OLA, hop % P == 0)
+// ===========================================================================
+
+__device__ __forceinline__ float norm_den(float w, int mode) {
+  return mode == TOMATIS_NORM_MAX ? fmaxf(w, 1e-8f) : (w + kEps32);
+}
+
+// wsum at position rel = p - first_start, frames in ascending order (bit-exact
+// with the reference's w_buf)
+__device__ float wsum_rel(int64_t rel, int64_t n_frames, int hop, int N, const float* win2) {
+  int64_t jhi = floordiv(rel, hop);
+  if (jhi > n_frames - 1) jhi = n_frames - 1;
+  int64_t jlo = floordiv(rel - N, hop) + 1;
+  if (jlo < 0) jlo = 0;
+  float w = 0.f;
+  for (int64_t j = jlo; j <= jhi; ++j) w = w + win2[rel - j * hop];
+  return w;
+}
+
+__device__ __forceinline__ int chunk_of(int64_t p, const TomatisStream& S) {
+  if (S.n_chunks <= 1 || p < S.chunk_first) return 0;
+  const int64_t c = 1 + (p - S.chunk_first) / S.chunk_len;
+  return (int)min<int64_t>(c, S.n_chunks - 1);
+}
+
+template <int P>
+__device__ __forceinline__ void flush_peak(float& pk, int cid, const TomatisStream& S,
+                                           uint32_t* peaks, int L, uint32_t* done) {
+  const float m = wave_max(pk);  // P > 64: each wave flushes its partial max
+  if ((L & 63) == 0) {
+    if (m > 0.f) atomicMax(peaks + S.chunk_base + cid, __float_as_uint(m));
+    if (done) {  // fused limiter: the max lands before the flush is counted
+      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(done + S.chunk_base + cid, 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  pk = 0.f;
+}
+
+// fused limiter tail of one wave: wait until every flush of chunk gc has been
+// counted (all contributors are dispatched no later than this wave's
+// neighbours), then scale this wave's own samples of the chunk.
+template <int CH>
+__device__ void limit_own(const MainArgs& A, const TomatisStream& S, int gc, int64_t lo,
+                          int64_t hi, int lane) {
+  const uint32_t need = A.chunk_need[gc];
+  uint32_t got = 0;
+  for (int spin = 0; spin < (1 << 18); ++spin) {
+    got = __hip_atomic_load(A.chunk_done + gc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    got = __builtin_amdgcn_readfirstlane(got);
+    if (got >= need) break;
+    __builtin_amdgcn_s_sleep(32);
+  }
+  if (got < need) {  // never expected; leaves the chunk unscaled and reports it
+    if (lane == 0) atomicOr(A.err, 1u);
+    return;
+  }
+  const float peak = __uint_as_float(__builtin_amdgcn_readfirstlane(
+      __hip_atomic_load(A.peaks + gc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+  if (!(peak > A.limit)) return;
+  const float sc = A.limit / peak;
+  const int64_t a = max(lo, A.chunk_rng[2 * gc]), b = min(hi, A.chunk_rng[2 * gc + 1]);
+  if (b <= a) return;
+  float* base = A.y + S.out_off + a * CH;
+  int64_t n = (b - a) * CH;
+  // scalar head up to 16-byte alignment, float4 body (16 in flight per lane), tail
+  const int head = (int)min<int64_t>(n, (4 - (int)((reinterpret_cast<uintptr_t>(base) >> 2) & 3)) & 3);
+  if (lane < head) base[lane] = base[lane] * sc;
+  base += head;
+  n -= head;
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  f4v* b4 = reinterpret_cast<f4v*>(base);
+  const int64_t n4 = n >> 2;
+  constexpr int U = 16;
+  for (int64_t i = lane; i < n4; i += 64 * U) {
+    f4v t[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i + 64 * u < n4) t[u] = __builtin_nontemporal_load(b4 + i + 64 * u);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i + 64 * u < n4) __builtin_nontemporal_store(t[u] * sc, b4 + i + 64 * u);
+  }
+  const int64_t t0 = n4 << 2;
+  if (t0 + lane < n) base[t0 + lane] = base[t0 + lane] * sc;
+}
+
+template <int CH>
+__device__ __forceinline__ cf load_cf(const float* xs, int64_t p) {
+  if constexpr (CH == 2) {
+    const float2 t = *reinterpret_cast<const float2*>(xs + 2 * p);
+    return {t.x, t.y};
+  } else {
+    return {xs[p], 0.f};
+  }
+}
+template <int CH>
+__device__ __forceinline__ void store_cf(float* ys, int64_t o, cf v) {
+  if constexpr (CH == 2) *reinterpret_cast<float2*>(ys + 2 * o) = make_float2(v.x, v.y);
+  else ys[o] = v.x;
+}
+template <int CH>
+__device__ __forceinline__ float cmag(cf v) {
+  if constexpr (CH == 2) return fmaxf(fabsf(v.x), fabsf(v.y));
+  else return fabsf(v.x);
+}
+
+// ---- buffer-resource memory ops: one 32-bit lane offset + SGPR/immediate offsets
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int f32x4 __attribute__((ext_vector_type(4)));  // raw b128 payload
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mk_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+// AUX: cache policy (gfx950: bit 1 = nt, streaming / evict-first)
+template <int CH, int AUX = 0>
+__device__ __forceinline__ cf bload(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  if constexpr (CH == 2) {
+    const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, AUX);
+    return {__uint_as_float(t.x), __uint_as_float(t.y)};
+  } else {
+    return {__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, AUX)), 0.f};
+  }
+}
+template <int CH, int AUX = 0>
+__device__ __forceinline__ void bstore(cf v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  if constexpr (CH == 2) {
+    const u32x2 t = {__float_as_uint(v.x), __float_as_uint(v.y)};
+    __builtin_amdgcn_raw_buffer_store_b64(t, r, voff, soff, AUX);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.x), r, voff, soff, AUX);
+  }
+}
+__device__ __forceinline__ float bloadf(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+
+// Fused framing -> window -> FFT -> gain -> IFFT -> window -> OLA -> normalise.
+// One sequence of P lanes (P/64 waves) processes frames [ka - (rmax-1), kb) of
+// one stream and emits the hop block of every frame >= ka.  Lane L register i
+// holds stream position s_k + L + P*i; the OLA accumulator for the next frame
+// is this frame's registers shifted by SH = hop/P.
+// GLDS: the (<= 2) gain rows live in LDS in the per-lane layout.
+template <int P, int NR, int SH, int CH, bool GLDS, bool PF, bool NT>
+__global__ __launch_bounds__(256, 2) void k_stft_ola(MainArgs A) {
+  using G = FftGeo<P, NR>;
+  constexpr int N = G::N;
+  constexpr int NSEQ = 256 / P;
+  constexpr int HOP = SH * P;
+  constexpr int NC = NR - SH;  // carried accumulator registers
+  constexpr int SHQ = (SH + 3) & ~3;  // winv registers padded to a quad
+  __shared__ __attribute__((aligned(16))) cf s_twN[NR * P];
+  __shared__ cf s_twP[P];
+  __shared__ __attribute__((aligned(16))) float s_win[N];      // lane-quad layout
+  __shared__ __attribute__((aligned(16))) float s_winv[SHQ * P];  // lane-quad layout
+  __shared__ cf s_buf[NSEQ][G::BUF];
+  __shared__ __attribute__((aligned(16))) float s_gain[GLDS ? 2 * N : 4];
+  for (int i = threadIdx.x; i < NR * P; i += 256) s_twN[i] = A.twN[i];
+  for (int i = threadIdx.x; i < P; i += 256) s_twP[i] = A.twP[i];
+  for (int e = threadIdx.x; e < N; e += 256) {  // e = lq(i, l)
+    const int q = e >> 2, l = q % P, i = (q / P) * 4 + (e & 3);
+    s_win[e] = A.win[l + P * i];
+  }
+  for (int e = threadIdx.x; e < SHQ * P; e += 256) {
+    const int q = e >> 2, l = q % P, i = (q / P) * 4 + (e & 3);
+    s_winv[e] = (i < SH) ? A.winv[l + P * i] : 0.f;
+  }
+  if constexpr (GLDS) {
+    const int nr = A.n_rows_lds;
+    for (int i = threadIdx.x; i < nr * N; i += 256) s_gain[i] = A.gains[i];
+  }
+  __syncthreads();
+  const float4* const w4 = reinterpret_cast<const float4*>(s_win);
+
+  const int seq = threadIdx.x / P, L = threadIdx.x % P;
+  // wave-uniform run id (readfirstlane: run and stream descriptors load as scalars)
+  const int run_id = __builtin_amdgcn_readfirstlane(blockIdx.x * NSEQ + seq);
+  Run R{0, 0, 0, 0};
+  const bool valid = run_id < A.n_runs;
+  if (valid) R = A.runs[run_id];
+  if constexpr (P <= 64) {
+    if (!valid) return;
+  }
+  const TomatisStream S = A.st[R.s];
+  const int64_t kfirst = max<int64_t>(0, R.ka - (A.rmax - 1));
+  int nit = valid ? (int)(R.kb - kfirst) : 0;
+  if constexpr (P > 64) {  // the block's sequences share barriers: same trip count
+    __shared__ int s_nit[NSEQ];
+    if (L == 0) s_nit[seq] = nit;
+    __syncthreads();
+    int m = 0;
+    for (int i = 0; i < NSEQ; ++i) m = max(m, s_nit[i]);
+    nit = m;
+  }
+  cf* buf = s_buf[seq];
+  const float* xs = A.x + S.in_off;
+  float* ys = A.y + S.out_off;
+  const int64_t out_end = S.out_begin + S.out_len;
+  const float oscale = S.out_scale;
+  const float iscale = S.in_scale;
+
+  if (valid && R.ka == 0 && S.first_start > S.out_begin) {  // adaptive: zeros before frame 0
+    for (int64_t p = S.out_begin + L; p < min(S.first_start, out_end); p += P)
+      store_cf<CH>(ys, p - S.out_begin, cf{0.f, 0.f});
+  }
+
+  // chunk tracking by frame index (host guarantees hop-aligned chunk boundaries)
+  const int64_t s_ka = S.first_start + R.ka * HOP;
+  int cid = chunk_of(s_ka, S);
+  const int cid_first = cid;
+  uint32_t* const done = (A.limit > 0.f) ? A.chunk_done : nullptr;
+  int64_t next_chunk_k = INT64_MAX;
+  if (S.n_chunks > 1 && cid < S.n_chunks - 1)
+    next_chunk_k = (S.chunk_first + (int64_t)cid * S.chunk_len - S.first_start) / HOP;
+  const int64_t chunk_k_step = S.n_chunks > 1 ? S.chunk_len / HOP : 0;
+  float pk = 0.f;
+
+  cf acc[NC];
+#pragma unroll
+  for (int i = 0; i < NC; ++i) acc[i] = {0.f, 0.f};
+
+  // frame loads are software-pipelined one frame ahead (the next frame's HBM/L2
+  // latency hides behind this frame's transforms)
+  auto load_frame = [&](int64_t kk, cf (&dst)[NR]) {
+    const bool lv = valid && (kk < R.kb);
+    const int64_t sk = S.first_start + kk * HOP;
+    if (lv && sk >= 0 && sk + N <= S.n) {
+      const __amdgpu_buffer_rsrc_t rx = mk_rsrc(xs + CH * sk, N * CH * 4);
+#pragma unroll
+      for (int n2 = 0; n2 < NR; ++n2) {
+        // the frame's first hop is read for the last time: stream it (nt)
+        if (NT && n2 < SH) dst[n2] = bload<CH, 2>(rx, L * CH * 4, P * n2 * CH * 4);
+        else dst[n2] = bload<CH>(rx, L * CH * 4, P * n2 * CH * 4);
+      }
+    } else {
+#pragma unroll
+      for (int n2 = 0; n2 < NR; ++n2) {
+        const int64_t p = sk + L + P * n2;
+        dst[n2] = (lv && p >= 0 && p < S.n) ? load_cf<CH>(xs, p) : cf{0.f, 0.f};
+      }
+    }
+  };
+  cf nx[NR];
+  if constexpr (PF) load_frame(kfirst, nx);
+
+  for (int it = 0; it < nit; ++it) {
+    const int64_t k = kfirst + it;
+    const bool live = valid && (k < R.kb);
+    const int64_t s_k = S.first_start + k * HOP;
+    const uint16_t row = live ? A.rows[S.frame_base + k] : 0;
+    cf v[NR];
+    if constexpr (PF) {
+#pragma unroll
+      for (int n2 = 0; n2 < NR; ++n2) v[n2] = nx[n2];
+      if (it + 1 < nit) load_frame(k + 1, nx);
+    } else {
+      load_frame(k, v);
+    }
+    // ---- analysis window (x * in_scale first, two roundings as the reference) ----
+    if (iscale != 1.0f) {
+#pragma unroll
+      for (int n2 = 0; n2 < NR; ++n2) v[n2] = cscale(v[n2], iscale);
+    }
+#pragma unroll
+    for (int n4 = 0; n4 < NR / 4; ++n4) {
+      const float4 w = w4[n4 * P + L];
+      v[4 * n4] = cscale(v[4 * n4], w.x);
+      v[4 * n4 + 1] = cscale(v[4 * n4 + 1], w.y);
+      v[4 * n4 + 2] = cscale(v[4 * n4 + 2], w.z);
+      v[4 * n4 + 3] = cscale(v[4 * n4 + 3], w.w);
+    }
+    fft_fwd<P, NR>(v, L, s_twN, s_twP, buf);
+    // ---- gain row (real, even, 1/N folded in), per-lane layout ----
+    if constexpr (GLDS) {
+      const float4* g4 = reinterpret_cast<const float4*>(s_gain + (row ? N : 0));
+#pragma unroll
+      for (int n4 = 0; n4 < NR / 4; ++n4) {
+        const float4 g = g4[n4 * P + L];
+        v[4 * n4] = cscale(v[4 * n4], g.x);
+        v[4 * n4 + 1] = cscale(v[4 * n4 + 1], g.y);
+        v[4 * n4 + 2] = cscale(v[4 * n4 + 2], g.z);
+        v[4 * n4 + 3] = cscale(v[4 * n4 + 3], g.w);
+      }
+    } else {
+      const __amdgpu_buffer_rsrc_t rg = mk_rsrc(A.gains + (int64_t)row * N, N * 4);
+#pragma unroll
+      for (int n4 = 0; n4 < NR / 4; ++n4) {
+        const f32x4 g = __builtin_amdgcn_raw_buffer_load_b128(rg, L * 16, n4 * P * 16, 0);
+        v[4 * n4] = cscale(v[4 * n4], __uint_as_float(g.x));
+        v[4 * n4 + 1] = cscale(v[4 * n4 + 1], __uint_as_float(g.y));
+        v[4 * n4 + 2] = cscale(v[4 * n4 + 2], __uint_as_float(g.z));
+        v[4 * n4 + 3] = cscale(v[4 * n4 + 3], __uint_as_float(g.w));
+      }
+    }
+    fft_inv<P, NR>(v, L, s_twN, s_twP, buf);
+    // ---- synthesis window fused with the register OLA ----
+#pragma unroll
+    for (int n4 = 0; n4 < NR / 4; ++n4) {
+      const float4 w = w4[n4 * P + L];
+      const float ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = 4 * n4 + u;
+        if (i < NC)
+          v[i] = {__builtin_fmaf(v[i].x, ww[u], acc[i].x), __builtin_fmaf(v[i].y, ww[u], acc[i].y)};
+        else
+          v[i] = cscale(v[i], ww[u]);
+      }
+    }
+    if (live && k >= R.ka) {
+      if (k == next_chunk_k) {
+        flush_peak<P>(pk, cid, S, A.peaks, L, done);
+        ++cid;
+        next_chunk_k = (cid < S.n_chunks - 1) ? next_chunk_k + chunk_k_step : INT64_MAX;
+      }
+      const bool full = (s_k >= S.out_begin) && (s_k + HOP <= out_end);
+      const bool edge = (k < A.rmax - 1);
+      if (full && !edge) {
+        const __amdgpu_buffer_rsrc_t ry = mk_rsrc(ys + CH * (s_k - S.out_begin), HOP * CH * 4);
+        float wv[SHQ];
+#pragma unroll
+        for (int q = 0; q < SHQ / 4; ++q) {
+          const float4 t = reinterpret_cast<const float4*>(s_winv)[q * P + L];
+          wv[4 * q] = t.x;
+          wv[4 * q + 1] = t.y;
+          wv[4 * q + 2] = t.z;
+          wv[4 * q + 3] = t.w;
+        }
+#pragma unroll
+        for (int i = 0; i < SH; ++i) {
+          const cf o = cscale(cscale(v[i], wv[i]), oscale);
+          if constexpr (NT) bstore<CH, 2>(o, ry, L * CH * 4, P * i * CH * 4);
+          else bstore<CH>(o, ry, L * CH * 4, P * i * CH * 4);
+          pk = fmaxf(pk, cmag<CH>(o));
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < SH; ++i) {
+          const int64_t p = s_k + L + P * i;
+          if (p >= S.out_begin && p < out_end) {
+            const float d = norm_den(wsum_rel(p - S.first_start, S.n_frames, HOP, N, A.win2),
+                                     A.norm_mode);
+            const cf o = cscale(cf{v[i].x / d, v[i].y / d}, oscale);
+            store_cf<CH>(ys, p - S.out_begin, o);
+            pk = fmaxf(pk, cmag<CH>(o));
+          }
+        }
+      }
+      if (R.last && k == R.kb - 1) {  // stream tail after the last frame
+#pragma unroll
+        for (int i = SH; i < NR; ++i) {
+          const int64_t p = s_k + L + P * i;
+          if (p >= S.out_begin && p < out_end) {
+            const float d = norm_den(wsum_rel(p - S.first_start, S.n_frames, HOP, N, A.win2),
+                                     A.norm_mode);
+            const cf o = cscale(cf{v[i].x / d, v[i].y / d}, oscale);
+            store_cf<CH>(ys, p - S.out_begin, o);
+            pk = fmaxf(pk, cmag<CH>(o));
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NC; ++i) acc[i] = v[i + SH];
+  }
+  if (valid) flush_peak<P>(pk, cid, S, A.peaks, L, done);
+  if (valid && done) {
+    // this wave's own output range (stores of frames [ka, kb) and the stream tail)
+    const int64_t s_last = S.first_start + (R.kb - 1) * HOP;
+    const int64_t lo = max(s_ka, S.out_begin) - S.out_begin;
+    const int64_t hi = min(s_last + (R.last ? (int64_t)N : (int64_t)HOP), out_end) - S.out_begin;
+    // P > 64: both waves of the sequence cover the same range; split it by wave
+    const int nw = P / 64, w = L >> 6;
+    const int64_t span = hi - lo, per = (span + nw - 1) / nw;
+    const int64_t wlo = lo + per * w, whi = min(hi, wlo + per);
+    for (int c = cid_first; c <= cid; ++c)
+      limit_own<CH>(A, S, S.chunk_base + c, wlo, whi, L & 63);
+  }
+}
+
+// Generic hop: same transform, windowed frame outputs to scratch, then a gather.
+template <int P, int NR>
+__global__ __launch_bounds__(256, 2) void k_stft_frames(MainArgs A) {
+  using G = FftGeo<P, NR>;
+  constexpr int N = G::N;
+  constexpr int NSEQ = 256 / P;
+  __shared__ __attribute__((aligned(16))) cf s_twN[NR * P];
+  __shared__ cf s_twP[P];
+  __shared__ float s_win[N];
+  __shared__ cf s_buf[NSEQ][G::BUF];
+  for (int i = threadIdx.x; i < NR * P; i += 256) s_twN[i] = A.twN[i];
+  for (int i = threadIdx.x; i < P; i += 256) s_twP[i] = A.twP[i];
+  for (int i = threadIdx.x; i < N; i += 256) s_win[i] = A.win[i];
+  __syncthreads();
+  const int seq = threadIdx.x / P, L = threadIdx.x % P;
+  const int run_id = blockIdx.x * NSEQ + seq;
+  Run R{0, 0, 0, 0};
+  const bool valid = run_id < A.n_runs;
+  if (valid) R = A.runs[run_id];
+  if constexpr (P <= 64) {
+    if (!valid) return;
+  }
+  const TomatisStream S = A.st[R.s];
+  int nit = valid ? (int)(R.kb - R.ka) : 0;
+  if constexpr (P > 64) {
+    __shared__ int s_nit[NSEQ];
+    if (L == 0) s_nit[seq] = nit;
+    __syncthreads();
+    int m = 0;
+    for (int i = 0; i < NSEQ; ++i) m = max(m, s_nit[i]);
+    nit = m;
+  }
+  cf* buf = s_buf[seq];
+  const float* xs = A.x + S.in_off;
+  const int hop = A.hop;
+  for (int it = 0; it < nit; ++it) {
+    const int64_t k = R.ka + it;
+    const bool live = valid && (k < R.kb);
+    const int64_t s_k = S.first_start + k * hop;
+    cf v[NR];
+#pragma unroll
+    for (int n2 = 0; n2 < NR; ++n2) {
+      const int64_t p = s_k + L + P * n2;
+      cf z = {0.f, 0.f};
+      if (live && p >= 0 && p < S.n) {
+        if (A.ch == 2) z = load_cf<2>(xs, p);
+        else z = load_cf<1>(xs, p);
+      }
+      const float w = s_win[L + P * n2];
+      v[n2] = {(z.x * S.in_scale) * w, (z.y * S.in_scale) * w};
+    }
+    fft_fwd<P, NR>(v, L, s_twN, s_twP, buf);
+    const uint16_t row = live ? A.rows[S.frame_base + k] : 0;
+    const float* g = A.gains + (int64_t)row * N;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) v[i] = cscale(v[i], g[lq<P>(i, L)]);
+    fft_inv<P, NR>(v, L, s_twN, s_twP, buf);
+    if (live) {
+      cf* dst = A.scratch + (S.frame_base + k) * (int64_t)N;
+#pragma unroll
+      for (int n2 = 0; n2 < NR; ++n2) dst[L + P * n2] = cscale(v[n2], s_win[L + P * n2]);
+    }
+  }
+}
+
+// gain rows [rows][n_bins] -> [rows][N] in the per-lane bin layout of fft_fwd,
+// mirrored (real even gain) and scaled by 1/N (exact: power of two)
+template <int P, int NR>
+__global__ void k_gain_perm(const float* __restrict__ g, int n_rows, int n_bins,
+                            float* __restrict__ out) {
+  constexpr int N = NR * P;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_rows * N) return;
+  const int row = t / N, e = t - row * N;  // e = lq(i, L)
+  const int q = e >> 2, L = q % P, i = (q / P) * 4 + (e & 3);
+  int b = fft_bin<P, NR>(L, i);
+  b = (b <= N / 2) ? b : N - b;
+  out[t] = g[(int64_t)row * n_bins + b] * (1.0f / (float)N);
+}
+
+// generic-hop OLA gather: one thread per output position (frame order preserved)
+__global__ __launch_bounds__(256) void k_ola_gather(MainArgs A, int n_streams,
+                                                    const int64_t* __restrict__ pos_base,
+                                                    int64_t total, int N) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  // stream lookup (binary search over position prefix)
+  int lo = 0, hi = n_streams - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) / 2;
+    if (pos_base[mid] <= t) lo = mid;
+    else hi = mid - 1;
+  }
+  const TomatisStream S = A.st[lo];
+  const int64_t p = S.out_begin + (t - pos_base[lo]);
+  const int hop = A.hop;
+  const int64_t rel = p - S.first_start;
+  int64_t jhi = floordiv(rel, hop);
+  if (jhi > S.n_frames - 1) jhi = S.n_frames - 1;
+  int64_t jlo = floordiv(rel - N, hop) + 1;
+  if (jlo < 0) jlo = 0;
+  float w = 0.f;
+  cf acc = {0.f, 0.f};
+  for (int64_t j = jlo; j <= jhi; ++j) {
+    const int off = (int)(rel - j * hop);
+    acc = acc + A.scratch[(S.frame_base + j) * (int64_t)N + off];
+    w = w + A.win2[off];
+  }
+  const float d = norm_den(w, A.norm_mode);
+  cf o = {acc.x / d, acc.y / d};
+  o = cscale(o, S.out_scale);
+  float* ys = A.y + S.out_off;
+  const int64_t oi = (p - S.out_begin) * A.ch;
+  if (A.ch == 2) *reinterpret_cast<float2*>(ys + oi) = make_float2(o.x, o.y);
+  else ys[oi] = o.x;
+  const float mag = (A.ch == 2) ? fmaxf(fabsf(o.x), fabsf(o.y)) : fabsf(o.x);
+  if (mag > 0.f) atomicMax(A.peaks + S.chunk_base + chunk_of(p, S), __float_as_uint(mag));
+}
+
+
+template <int P, int NR, int SH, bool PF, bool NT>
+void launch_main_pf(const MainArgs& A, int ch, int nseq_blocks, hipStream_t s) {
+  const bool gl = A.n_rows_lds > 0;
+  if (ch == 2) {
+    if (gl) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, true, PF, NT>), dim3(nseq_blocks), dim3(256), 0, s, A);
+    else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, false, PF, NT>), dim3(nseq_blocks), dim3(256), 0, s, A);
+  } else {
+    if (gl) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, true, PF, NT>), dim3(nseq_blocks), dim3(256), 0, s, A);
+    else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, false, PF, NT>), dim3(nseq_blocks), dim3(256), 0, s, A);
+  }
+}
+template <int P, int NR, int SH>
+void launch_main(const MainArgs& A, int ch, int nseq_blocks, hipStream_t s) {
+  // frame prefetch pays for NR = 16 (2 waves/SIMD kept); NR = 32 is register-bound.
+  // Streaming (nt) hints on last-use input and on output keep the frame overlap
+  // resident in L2 (FETCH_SIZE 4.5 -> 1.8 GB per C2 launch at P = 64).
+  launch_main_pf<P, NR, SH, NR == 16, true>(A, ch, nseq_blocks, s);
+}
+
+}  // namespace
+
+namespace tshared {
+
+void launch_transform(const MainArgs& A, int P, int NR, int SH, int ch, int blocks, hipStream_t s) {
+  if (P == 64) {
+    if (SH == 4) launch_main<64, 32, 4>(A, ch, blocks, s);
+    else if (SH == 8) launch_main<64, 32, 8>(A, ch, blocks, s);
+    else launch_main<64, 32, 16>(A, ch, blocks, s);
+  } else if (NR == 16) {
+    if (SH == 2) launch_main<128, 16, 2>(A, ch, blocks, s);
+    else if (SH == 4) launch_main<128, 16, 4>(A, ch, blocks, s);
+    else launch_main<128, 16, 8>(A, ch, blocks, s);
+  } else {
+    if (SH == 4) launch_main<128, 32, 4>(A, ch, blocks, s);
+    else if (SH == 8) launch_main<128, 32, 8>(A, ch, blocks, s);
+    else launch_main<128, 32, 16>(A, ch, blocks, s);
+  }
+}
+
+void launch_frames(const MainArgs& A, int P, int NR, int blocks, hipStream_t s) {
+  if (P == 64) hipLaunchKernelGGL((k_stft_frames<64, 32>), dim3(blocks), dim3(256), 0, s, A);
+  else if (NR == 16) hipLaunchKernelGGL((k_stft_frames<128, 16>), dim3(blocks), dim3(256), 0, s, A);
+  else hipLaunchKernelGGL((k_stft_frames<128, 32>), dim3(blocks), dim3(256), 0, s, A);
+}
+
+void launch_gain_perm(int P, int NR, const float* gains, int n_rows, int n_bins, float* out,
+                      hipStream_t s) {
+  const int N = P * NR;
+  const int nb = (n_rows * N + 255) / 256;
+  if (P == 64)
+    hipLaunchKernelGGL((k_gain_perm<64, 32>), dim3(nb), dim3(256), 0, s, gains, n_rows, n_bins, out);
+  else if (NR == 16)
+    hipLaunchKernelGGL((k_gain_perm<128, 16>), dim3(nb), dim3(256), 0, s, gains, n_rows, n_bins, out);
+  else
+    hipLaunchKernelGGL((k_gain_perm<128, 32>), dim3(nb), dim3(256), 0, s, gains, n_rows, n_bins, out);
+}
+
+void launch_ola_gather(const MainArgs& A, int n_streams, const int64_t* pos_base, int64_t total,
+                       int N, hipStream_t s) {
+  const int64_t ng = (total + 255) / 256;
+  hipLaunchKernelGGL(k_ola_gather, dim3((unsigned)ng), dim3(256), 0, s, A, n_streams, pos_base,
+                     total, N);
+}
+
+}  // namespace tshared
