@@ -18,9 +18,11 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
+# machine scheduler of the transform unit ("" = LLVM's default, occupancy-aware)
+SCHED = os.environ.get("TOMATIS_TRANSFORM_SCHED", "")
 UNITS = {  # source -> extra flags
     "tm_kernels.hip": [],
-    "tm_transform.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+    "tm_transform.hip": ["-mllvm", f"-amdgpu-sched-strategy={SCHED}"] if SCHED else [],
 }
 DEPS = [os.path.join(CSRC, f) for f in (*UNITS, "tm_common.h", "tm_fft.h", "tm_shared.h")] + \
        [os.path.join(ROOT, "include", "tomatis_hip.h")]

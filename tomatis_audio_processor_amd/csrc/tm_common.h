@@ -146,6 +146,16 @@ __device__ __forceinline__ void dft(cf (&v)[NT]) {
 // ---------------------------------------------------------------------------
 // misc
 // ---------------------------------------------------------------------------
+// an opaque copy of a lane value: values derived from it inside a rarely taken
+// branch are computed there, instead of being hoisted out of the frame loop by
+// LICM and kept live in VGPRs for the whole kernel (the edge-frame addresses
+// alone cost 64 VGPRs, i.e. a wave of occupancy)
+__device__ __forceinline__ int opaque(int v) {
+  int r;
+  __asm__ volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(v));
+  return r;
+}
+
 __device__ __forceinline__ float wave_max(float v) {
   for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
   return v;

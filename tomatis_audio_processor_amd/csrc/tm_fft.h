@@ -19,6 +19,15 @@
 
 namespace tdsp {
 
+// scheduling fence between FFT steps: keeps each step's LDS table reads next to
+// their use instead of hoisted a whole step ahead (register pressure; the other
+// waves on the SIMD hide the latency)
+#if defined(TM_SB)
+#define TM_STEP_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define TM_STEP_FENCE()
+#endif
+
 template <int P_, int NR_ = 32>
 struct FftGeo {
   static constexpr int P = P_;
@@ -35,6 +44,9 @@ struct FftGeo {
 // LDS synchronisation for an exchange: wave-local when P == 64.
 template <int P>
 __device__ __forceinline__ void xsync() {
+#ifdef TM_EXP_NOSYNC  // timing experiments only (wrong results): no exchange ordering
+  if constexpr (P <= 64) return;
+#endif
   if constexpr (P <= 64) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -50,7 +62,10 @@ __device__ __forceinline__ int x2col(int a, int c) { return 8 * c + (a ^ (c & 7)
 // forward FFT.  v: 32 registers (input x[L + P*n2]); out: bin layout above.
 // twN: LDS W_N^{n1*k2} in lane-pair layout [k2/2][n1][k2&1] (16-B aligned);
 // twP: LDS [P] with W_P^m; buf: round buffer.
-template <int P, int NR = 32>
+// LT: twP is the per-lane table W_P^{(L%8)*m} for m < 8 in lane-pair layout
+// [m/2][L][m&1] (P == 64 only: one ds_read_b128 per two twiddles, one address
+// VGPR instead of seven)
+template <int P, int NR = 32, bool LT = false>
 __device__ __forceinline__ void fft_fwd(cf (&v)[NR], int L, const cf* twN, const cf* twP,
                                         cf* buf) {
   using G = FftGeo<P, NR>;
@@ -59,6 +74,7 @@ __device__ __forceinline__ void fft_fwd(cf (&v)[NR], int L, const cf* twN, const
   const int c3 = L % PB, q3 = L / PB;
   // step 1
   dft<NR, false, 0, 1, NR>(v);
+  TM_STEP_FENCE();
   // step 2 (twiddles in lane-pair layout: one ds_read_b128 per two registers)
   sfor<0, NR / 2>([&](auto kk) {
     constexpr int K2 = decltype(kk)::value;
@@ -80,20 +96,35 @@ __device__ __forceinline__ void fft_fwd(cf (&v)[NR], int L, const cf* twN, const
     });
     xsync<P>();
   });
+  TM_STEP_FENCE();
   // step 3a: DFT_PB over b for each j
   sfor<0, G::NJ>([&](auto jj) {
     constexpr int J = decltype(jj)::value;
     dft<PB, false, J * PB, 1, NR>(v);
   });
+  TM_STEP_FENCE();
   // step 3b: W_P^{a c}
-  sfor<1, PB>([&](auto cc) {
-    constexpr int C = decltype(cc)::value;
-    const cf w = twP[(a1 * C) & (P - 1)];
-    sfor<0, G::NJ>([&](auto jj) {
-      constexpr int J = decltype(jj)::value;
-      v[J * PB + C] = cmul(v[J * PB + C], w);
+  if constexpr (LT) {
+    static_assert(PB == 8, "lane twiddle table needs P == 64");
+    sfor<0, 4>([&](auto cc) {
+      constexpr int C2 = decltype(cc)::value;
+      const float4 t = reinterpret_cast<const float4*>(twP)[C2 * P + L];
+      sfor<0, G::NJ>([&](auto jj) {
+        constexpr int J = decltype(jj)::value;
+        if constexpr (C2 > 0) v[J * PB + 2 * C2] = cmul(v[J * PB + 2 * C2], cf{t.x, t.y});
+        v[J * PB + 2 * C2 + 1] = cmul(v[J * PB + 2 * C2 + 1], cf{t.z, t.w});
+      });
     });
-  });
+  } else {
+    sfor<1, PB>([&](auto cc) {
+      constexpr int C = decltype(cc)::value;
+      const cf w = twP[(a1 * C) & (P - 1)];
+      sfor<0, G::NJ>([&](auto jj) {
+        constexpr int J = decltype(jj)::value;
+        v[J * PB + C] = cmul(v[J * PB + C], w);
+      });
+    });
+  }
   // exchange 2 : (lane (a,q), reg (j,c)) -> (lane (c,q'), reg (j',a))
   sfor<0, G::ROUNDS>([&](auto rr) {
     constexpr int R = decltype(rr)::value;
@@ -112,6 +143,7 @@ __device__ __forceinline__ void fft_fwd(cf (&v)[NR], int L, const cf* twN, const
     });
     xsync<P>();
   });
+  TM_STEP_FENCE();
   // step 3c: DFT_8 over a
   sfor<0, NR / 8>([&](auto jj) {
     constexpr int J = decltype(jj)::value;
@@ -120,7 +152,7 @@ __device__ __forceinline__ void fft_fwd(cf (&v)[NR], int L, const cf* twN, const
 }
 
 // inverse (unnormalised) FFT: bin layout -> v[n2] = x[L + P*n2] * N
-template <int P, int NR = 32>
+template <int P, int NR = 32, bool LT = false>
 __device__ __forceinline__ void fft_inv(cf (&v)[NR], int L, const cf* twN, const cf* twP,
                                         cf* buf) {
   using G = FftGeo<P, NR>;
@@ -132,15 +164,28 @@ __device__ __forceinline__ void fft_inv(cf (&v)[NR], int L, const cf* twN, const
     constexpr int J = decltype(jj)::value;
     dft<8, true, J * 8, 1, NR>(v);
   });
+  TM_STEP_FENCE();
   // step 3b': conj W_P^{a c3}
-  sfor<1, 8>([&](auto aa) {
-    constexpr int A = decltype(aa)::value;
-    const cf w = twP[(A * c3) & (P - 1)];
-    sfor<0, NR / 8>([&](auto jj) {
-      constexpr int J = decltype(jj)::value;
-      v[J * 8 + A] = cmulc(v[J * 8 + A], w);
+  if constexpr (LT) {  // c3 = L % 8 here: same table as the forward step 3b
+    sfor<0, 4>([&](auto aa) {
+      constexpr int A2 = decltype(aa)::value;
+      const float4 t = reinterpret_cast<const float4*>(twP)[A2 * P + L];
+      sfor<0, NR / 8>([&](auto jj) {
+        constexpr int J = decltype(jj)::value;
+        if constexpr (A2 > 0) v[J * 8 + 2 * A2] = cmulc(v[J * 8 + 2 * A2], cf{t.x, t.y});
+        v[J * 8 + 2 * A2 + 1] = cmulc(v[J * 8 + 2 * A2 + 1], cf{t.z, t.w});
+      });
     });
-  });
+  } else {
+    sfor<1, 8>([&](auto aa) {
+      constexpr int A = decltype(aa)::value;
+      const cf w = twP[(A * c3) & (P - 1)];
+      sfor<0, NR / 8>([&](auto jj) {
+        constexpr int J = decltype(jj)::value;
+        v[J * 8 + A] = cmulc(v[J * 8 + A], w);
+      });
+    });
+  }
   // exchange 3 : (lane (c,q'), reg (j',a)) -> (lane (a,q), reg (j,c))
   sfor<0, G::ROUNDS>([&](auto rr) {
     constexpr int R = decltype(rr)::value;
@@ -159,6 +204,7 @@ __device__ __forceinline__ void fft_inv(cf (&v)[NR], int L, const cf* twN, const
     });
     xsync<P>();
   });
+  TM_STEP_FENCE();
   // step 3a': IDFT_PB over c -> b
   sfor<0, G::NJ>([&](auto jj) {
     constexpr int J = decltype(jj)::value;
@@ -178,6 +224,7 @@ __device__ __forceinline__ void fft_inv(cf (&v)[NR], int L, const cf* twN, const
     });
     xsync<P>();
   });
+  TM_STEP_FENCE();
   // step 2': conj W_N^{n1 k2}
   sfor<0, NR / 2>([&](auto kk) {
     constexpr int K2 = decltype(kk)::value;
@@ -185,6 +232,7 @@ __device__ __forceinline__ void fft_inv(cf (&v)[NR], int L, const cf* twN, const
     if constexpr (K2 > 0) v[2 * K2] = cmulc(v[2 * K2], cf{t.x, t.y});
     v[2 * K2 + 1] = cmulc(v[2 * K2 + 1], cf{t.z, t.w});
   });
+  TM_STEP_FENCE();
   // step 1': IDFT_NR over k2 -> n2
   dft<NR, true, 0, 1, NR>(v);
 }

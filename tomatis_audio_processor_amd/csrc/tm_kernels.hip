@@ -887,22 +887,93 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
   if ((rc = dalloc_copy(&p->st, p->hs))) return rc;
   // --- main-kernel runs ---
   const int64_t tf_total = std::max<int64_t>(1, p->total_frames);
+  // Runs.  Per stream, the emitted frames [e_lo, e_hi) whose run can take the
+  // fused kernel's interior loop (full frame loads back to the warm-up frames,
+  // full interior output blocks, not the stream's last frame) are cut into
+  // equal runs; the few edge frames before/after form one generic run each.
+  // One run per resident sequence slot of the fused kernel (a single wave of
+  // blocks, every wave busy to the end), at least 48 frames per interior run
+  // so the rmax-1 warm-up frames per run stay a few percent.
+  const int rmax_ = (N + hop - 1) / hop;
+  const bool fast_ok = !p->generic && P == 64 && env_int("TOMATIS_FAST_LOOP", 1) != 0;
+  std::vector<int64_t> e_lo(ns, 0), e_hi(ns, 0);
+  int64_t fast_total = 0, n_edge = 0;
+  for (int s = 0; s < ns; ++s) {
+    const TomatisStream& S = p->hs[s];
+    const int64_t F = S.n_frames;
+    int64_t lo = F, hi = F;
+    if (fast_ok && F > 0) {
+      auto sk = [&](int64_t k) { return S.first_start + k * hop; };
+      auto ceil_div = [](int64_t a_, int64_t b_) { return a_ >= 0 ? (a_ + b_ - 1) / b_ : -((-a_) / b_); };
+      lo = rmax_ - 1;                                                   // not an edge frame
+      lo = std::max(lo, ceil_div(S.out_begin - S.first_start, hop));     // s_k >= out_begin
+      lo = std::max(lo, ceil_div(-S.first_start, hop) + rmax_ - 1);      // warm-up frames load fully
+      // s_k + hop <= out_end, s_k + N <= n, k <= F - 2
+      hi = F - 1;
+      const int64_t out_end = S.out_begin + S.out_len;
+      auto fdiv = [](int64_t a_, int64_t b_) { return a_ >= 0 ? a_ / b_ : -((-a_ + b_ - 1) / b_); };
+      hi = std::min(hi, fdiv(out_end - hop - S.first_start, hop) + 1);
+      hi = std::min(hi, fdiv(S.n - N - S.first_start, hop) + 1);
+      lo = std::max<int64_t>(0, lo);
+      if (hi - lo < 48) lo = hi = F;  // too short: all generic
+      else {
+        (void)sk;
+        n_edge += (lo > 0) + (hi < F);
+      }
+    }
+    e_lo[s] = lo;
+    e_hi[s] = hi;
+    fast_total += hi - lo;
+  }
   int T = env_int("TOMATIS_RUN_FRAMES", 0);
   if (T <= 0) {
-    const int64_t target = 4096;
-    T = (int)std::max<int64_t>(48, (tf_total + target - 1) / target);
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+      (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const int64_t slots = (int64_t)std::max(1, ncu) *
+                          (p->generic ? 8 : transform_slots_per_cu(P, p->NR));
+    // generic streams and the edge runs take slots first
+    int64_t gen_frames = 0;
+    for (int s = 0; s < ns; ++s)
+      if (e_lo[s] == e_hi[s]) gen_frames += p->hs[s].n_frames;
+    const int64_t work = fast_total + gen_frames;
+    const int64_t avail = std::max<int64_t>(1, slots - n_edge);
+    T = (int)std::max<int64_t>(48, (work + avail - 1) / avail);
+    auto count = [&](int64_t t) {
+      int64_t c = n_edge;
+      for (int s = 0; s < ns; ++s) {
+        const int64_t len = (e_lo[s] == e_hi[s]) ? p->hs[s].n_frames : e_hi[s] - e_lo[s];
+        c += (len + t - 1) / t;
+      }
+      return c;
+    };
+    while (count(T) > slots && T < tf_total) T += std::max(1, T / 64);
   }
+  T = std::min(T, 1 << 20);  // interior buffer resources stay far below 4 GB
   std::vector<Run> runs;
-  for (int s = 0; s < ns; ++s) {
-    const int64_t F = p->hs[s].n_frames;
-    for (int64_t a = 0; a < F; a += T) {
+  auto add_runs = [&](int s, int64_t a0, int64_t a1, int32_t flags) {
+    // equal cuts of [a0, a1) into ceil(len / T) runs
+    const int64_t len = a1 - a0;
+    if (len <= 0) return;
+    const int64_t nr = (len + T - 1) / T;
+    for (int64_t j = 0; j < nr; ++j) {
       Run r;
       r.s = s;
-      r.ka = a;
-      r.kb = std::min<int64_t>(F, a + T);
-      r.last = (r.kb == F) ? 1 : 0;
+      r.ka = a0 + len * j / nr;
+      r.kb = a0 + len * (j + 1) / nr;
+      r.last = flags | ((r.kb == p->hs[s].n_frames) ? 1 : 0);
       runs.push_back(r);
     }
+  };
+  for (int s = 0; s < ns; ++s) {
+    const int64_t F = p->hs[s].n_frames;
+    if (e_lo[s] == e_hi[s]) {
+      add_runs(s, 0, F, 0);
+      continue;
+    }
+    if (e_lo[s] > 0) add_runs(s, 0, e_lo[s], 0);
+    add_runs(s, e_lo[s], e_hi[s], kRunInterior);
+    if (e_hi[s] < F) add_runs(s, e_hi[s], F, 0);
   }
   p->n_runs = (int)runs.size();
   if ((rc = dalloc_copy(&p->runs, runs))) return rc;
@@ -1348,6 +1419,7 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
   A.chunk_need = p->chunk_need;
   A.chunk_rng = p->chunk_rng;
   A.err = p->err;
+  A.prof = nullptr;
   if (limit > 0.f) {
     if (!p->chunk_done) return TOMATIS_E_UNSUPPORTED;
     if (hipMemsetAsync(p->chunk_done, 0, (size_t)p->total_chunks * 4, s)) return TOMATIS_E_HIP;
@@ -1362,7 +1434,27 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
     launch_ola_gather(A, p->n_streams, p->pos_base, p->total_out, N, s);
     return launch_check();
   }
-  launch_transform(A, p->P, p->NR, p->SH, ch, blocks, s);
+#ifdef TM_PROFILE
+  static unsigned long long* prof = nullptr;
+  if (!prof) (void)hipMalloc(reinterpret_cast<void**>(&prof), 16 * sizeof(unsigned long long));
+  (void)hipMemsetAsync(prof, 0, 16 * sizeof(unsigned long long), s);
+  A.prof = prof;
+  launch_transform(A, p->P, p->NR, p->SH, ch, transform_wg(p->P, p->NR), s);
+  {
+    unsigned long long h[16];
+    (void)hipMemcpyAsync(h, prof, sizeof(h), hipMemcpyDeviceToHost, s);
+    (void)hipStreamSynchronize(s);
+    const double fr = h[15] ? (double)h[15] : 1.0;
+    fprintf(stderr, "[tm_profile] frames %llu cycles/frame: top %.0f win %.0f fwd %.0f gain %.0f inv %.0f synth %.0f emit %.0f\n",
+            h[15], h[0] / fr, h[1] / fr, h[2] / fr, h[3] / fr, h[4] / fr, h[5] / fr, h[6] / fr);
+    const double nw = h[10] ? (double)h[10] : 1.0;
+    fprintf(stderr, "[tm_profile] waves %llu prologue %.0f lifetime %.0f cycles, %.1f us, clock %.2f GHz, loop share %.3f\n",
+            h[10], h[7] / nw, h[8] / nw, h[9] / nw / 100.0, h[9] ? (double)h[8] / (double)h[9] * 0.1 : 0.0,
+            (h[0] + h[1] + h[2] + h[3] + h[4] + h[5] + h[6]) / (double)(h[8] ? h[8] : 1));
+  }
+  return launch_check();
+#endif
+  launch_transform(A, p->P, p->NR, p->SH, ch, transform_wg(p->P, p->NR), s);
   return launch_check();
 }
 

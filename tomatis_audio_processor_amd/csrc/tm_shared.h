@@ -16,9 +16,12 @@ constexpr double kEps64 = 1e-12;
 
 struct Run {          // main-kernel work item: emit frames [ka, kb) of stream s
   int32_t s;
-  int32_t last;       // 1 if kb is the stream's last frame + 1
+  int32_t last;       // bit 0: kb is the stream's last frame + 1; bit 1: kRunInterior
   int64_t ka, kb;
 };
+// interior run: frames [max(0, ka - rmax + 1), kb) all read full frames and every
+// emitted hop block is a full interior block (fast loop of the fused kernel)
+constexpr int32_t kRunInterior = 2;
 
 __device__ __forceinline__ int64_t floordiv(int64_t a, int64_t b) {
   int64_t q = a / b;
@@ -48,10 +51,13 @@ struct MainArgs {
   const uint32_t* chunk_need;
   const int64_t* chunk_rng;  // [2 * chunk]: output-relative [p0, p1)
   uint32_t* err;
+  unsigned long long* prof;  // TM_PROFILE builds only: per-phase wave cycles
 };
 
 // launchers (tm_transform.hip); kernels stay private to that unit
-void launch_transform(const MainArgs& A, int P, int NR, int SH, int ch, int blocks, hipStream_t s);
+int transform_wg(int P, int NR);  // workgroup size of the fused kernel
+int transform_slots_per_cu(int P, int NR);  // resident sequences per CU
+void launch_transform(const MainArgs& A, int P, int NR, int SH, int ch, int wg, hipStream_t s);
 void launch_frames(const MainArgs& A, int P, int NR, int blocks, hipStream_t s);
 void launch_gain_perm(int P, int NR, const float* gains, int n_rows, int n_bins, float* out,
                       hipStream_t s);

@@ -16,6 +16,17 @@ using namespace tdsp;
 using namespace tshared;
 
 namespace {
+#ifdef TM_PROFILE  // diagnostic builds: per-phase wave cycles of the interior loop
+#define TPROF(i, dep)                                              \
+  {                                                                \
+    __asm__ volatile("" ::"v"(dep));                               \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();    \
+    tacc[i] += t_ - tlast;                                         \
+    tlast = t_;                                                    \
+  }
+#else
+#define TPROF(i, dep)
+#endif
 // ===========================================================================
 // Fused STFT -> gain -> ISTFT -> OLA -> normalise (register OLA, hop % P == 0)
 // ===========================================================================
@@ -154,42 +165,61 @@ __device__ __forceinline__ float bloadf(__amdgpu_buffer_rsrc_t r, int voff, int 
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
 }
 
+// read-only (for the kernel's lifetime) data through the scalar cache: a
+// constant-address-space view makes uniform loads s_load (lgkmcnt-counted)
+typedef __attribute__((address_space(4))) const uint32_t cu32;
+
 // Fused framing -> window -> FFT -> gain -> IFFT -> window -> OLA -> normalise.
 // One sequence of P lanes (P/64 waves) processes frames [ka - (rmax-1), kb) of
 // one stream and emits the hop block of every frame >= ka.  Lane L register i
 // holds stream position s_k + L + P*i; the OLA accumulator for the next frame
 // is this frame's registers shifted by SH = hop/P.
 // GLDS: the (<= 2) gain rows live in LDS in the per-lane layout.
-template <int P, int NR, int SH, int CH, bool GLDS, bool PF, bool NT>
-__global__ __launch_bounds__(256, 2) void k_stft_ola(MainArgs A) {
+template <int P, int NR, int SH, int CH, bool GLDS, bool PF, bool NT, int WG>
+__global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(MainArgs A) {
+#ifdef TM_PROFILE
+  const unsigned long long t_k0 = __builtin_amdgcn_s_memtime();
+  const unsigned long long rt_k0 = __builtin_amdgcn_s_memrealtime();
+#endif
   using G = FftGeo<P, NR>;
   constexpr int N = G::N;
-  constexpr int NSEQ = 256 / P;
+  constexpr int NSEQ = WG / P;
   constexpr int HOP = SH * P;
   constexpr int NC = NR - SH;  // carried accumulator registers
   constexpr int SHQ = (SH + 3) & ~3;  // winv registers padded to a quad
+  constexpr bool LT = P == 64;  // per-lane step-3 twiddle table
   __shared__ __attribute__((aligned(16))) cf s_twN[NR * P];
-  __shared__ cf s_twP[P];
+  __shared__ __attribute__((aligned(16))) cf s_twP[LT ? 8 * P : P];
   __shared__ __attribute__((aligned(16))) float s_win[N];      // lane-quad layout
   __shared__ __attribute__((aligned(16))) float s_winv[SHQ * P];  // lane-quad layout
   __shared__ cf s_buf[NSEQ][G::BUF];
   __shared__ __attribute__((aligned(16))) float s_gain[GLDS ? 2 * N : 4];
-  for (int i = threadIdx.x; i < NR * P; i += 256) s_twN[i] = A.twN[i];
-  for (int i = threadIdx.x; i < P; i += 256) s_twP[i] = A.twP[i];
-  for (int e = threadIdx.x; e < N; e += 256) {  // e = lq(i, l)
+  for (int i = threadIdx.x; i < NR * P; i += WG) s_twN[i] = A.twN[i];
+  if constexpr (LT) {  // [m/2][l][m&1] = W_P^{(l%8)*m}
+    for (int i = threadIdx.x; i < 8 * P; i += WG) {
+      const int m = 2 * (i / (2 * P)) + (i & 1), l = (i / 2) % P;
+      s_twP[i] = A.twP[((l & 7) * m) & (P - 1)];
+    }
+  } else {
+    for (int i = threadIdx.x; i < P; i += WG) s_twP[i] = A.twP[i];
+  }
+  for (int e = threadIdx.x; e < N; e += WG) {  // e = lq(i, l)
     const int q = e >> 2, l = q % P, i = (q / P) * 4 + (e & 3);
     s_win[e] = A.win[l + P * i];
   }
-  for (int e = threadIdx.x; e < SHQ * P; e += 256) {
+  for (int e = threadIdx.x; e < SHQ * P; e += WG) {
     const int q = e >> 2, l = q % P, i = (q / P) * 4 + (e & 3);
     s_winv[e] = (i < SH) ? A.winv[l + P * i] : 0.f;
   }
   if constexpr (GLDS) {
     const int nr = A.n_rows_lds;
-    for (int i = threadIdx.x; i < nr * N; i += 256) s_gain[i] = A.gains[i];
+    for (int i = threadIdx.x; i < nr * N; i += WG) s_gain[i] = A.gains[i];
   }
   __syncthreads();
   const float4* const w4 = reinterpret_cast<const float4*>(s_win);
+#ifdef TM_PROFILE
+  const unsigned long long t_k1 = __builtin_amdgcn_s_memtime();
+#endif
 
   const int seq = threadIdx.x / P, L = threadIdx.x % P;
   // wave-uniform run id (readfirstlane: run and stream descriptors load as scalars)
@@ -238,156 +268,312 @@ __global__ __launch_bounds__(256, 2) void k_stft_ola(MainArgs A) {
 #pragma unroll
   for (int i = 0; i < NC; ++i) acc[i] = {0.f, 0.f};
 
-  // frame loads are software-pipelined one frame ahead (the next frame's HBM/L2
-  // latency hides behind this frame's transforms)
-  auto load_frame = [&](int64_t kk, cf (&dst)[NR]) {
-    const bool lv = valid && (kk < R.kb);
-    const int64_t sk = S.first_start + kk * HOP;
-    if (lv && sk >= 0 && sk + N <= S.n) {
-      const __amdgpu_buffer_rsrc_t rx = mk_rsrc(xs + CH * sk, N * CH * 4);
-#pragma unroll
-      for (int n2 = 0; n2 < NR; ++n2) {
-        // the frame's first hop is read for the last time: stream it (nt)
-        if (NT && n2 < SH) dst[n2] = bload<CH, 2>(rx, L * CH * 4, P * n2 * CH * 4);
-        else dst[n2] = bload<CH>(rx, L * CH * 4, P * n2 * CH * 4);
+#ifdef TM_PROFILE
+  unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tlast = __builtin_amdgcn_s_memtime();
+#endif
+  // window -> FFT -> gain row -> IFFT -> window, OLA into the accumulator
+  auto transform = [&](cf (&v)[NR], uint32_t row) {
+      // ---- analysis window (x * in_scale first, two roundings as the reference) ----
+      if (iscale != 1.0f) {
+  #pragma unroll
+        for (int n2 = 0; n2 < NR; ++n2) v[n2] = cscale(v[n2], iscale);
       }
-    } else {
-#pragma unroll
-      for (int n2 = 0; n2 < NR; ++n2) {
-        const int64_t p = sk + L + P * n2;
-        dst[n2] = (lv && p >= 0 && p < S.n) ? load_cf<CH>(xs, p) : cf{0.f, 0.f};
+  #pragma unroll
+      for (int n4 = 0; n4 < NR / 4; ++n4) {
+        const float4 w = w4[n4 * P + L];
+        v[4 * n4] = cscale(v[4 * n4], w.x);
+        v[4 * n4 + 1] = cscale(v[4 * n4 + 1], w.y);
+        v[4 * n4 + 2] = cscale(v[4 * n4 + 2], w.z);
+        v[4 * n4 + 3] = cscale(v[4 * n4 + 3], w.w);
       }
+      TPROF(1, v[NR - 1].x);
+      fft_fwd<P, NR, LT>(v, L, s_twN, s_twP, buf);
+      TPROF(2, v[NR - 1].x);
+      // ---- gain row (real, even, 1/N folded in), per-lane layout ----
+      if constexpr (GLDS) {
+        const float4* g4 = reinterpret_cast<const float4*>(s_gain + (row ? N : 0));
+  #pragma unroll
+        for (int n4 = 0; n4 < NR / 4; ++n4) {
+          const float4 g = g4[n4 * P + L];
+          v[4 * n4] = cscale(v[4 * n4], g.x);
+          v[4 * n4 + 1] = cscale(v[4 * n4 + 1], g.y);
+          v[4 * n4 + 2] = cscale(v[4 * n4 + 2], g.z);
+          v[4 * n4 + 3] = cscale(v[4 * n4 + 3], g.w);
+        }
+      } else {
+        const __amdgpu_buffer_rsrc_t rg = mk_rsrc(A.gains + (int64_t)row * N, N * 4);
+  #pragma unroll
+        for (int n4 = 0; n4 < NR / 4; ++n4) {
+          const f32x4 g = __builtin_amdgcn_raw_buffer_load_b128(rg, L * 16, n4 * P * 16, 0);
+          v[4 * n4] = cscale(v[4 * n4], __uint_as_float(g.x));
+          v[4 * n4 + 1] = cscale(v[4 * n4 + 1], __uint_as_float(g.y));
+          v[4 * n4 + 2] = cscale(v[4 * n4 + 2], __uint_as_float(g.z));
+          v[4 * n4 + 3] = cscale(v[4 * n4 + 3], __uint_as_float(g.w));
+        }
+      }
+      TPROF(3, v[NR - 1].x);
+      fft_inv<P, NR, LT>(v, L, s_twN, s_twP, buf);
+      TPROF(4, v[NR - 1].x);
+      // ---- synthesis window fused with the register OLA ----
+  #pragma unroll
+      for (int n4 = 0; n4 < NR / 4; ++n4) {
+        const float4 w = w4[n4 * P + L];
+        const float ww[4] = {w.x, w.y, w.z, w.w};
+  #pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int i = 4 * n4 + u;
+          if (i < NC)
+            v[i] = {__builtin_fmaf(v[i].x, ww[u], acc[i].x), __builtin_fmaf(v[i].y, ww[u], acc[i].y)};
+          else
+            v[i] = cscale(v[i], ww[u]);
+        }
+      }
+  };
+  // the first SH registers of an emitted frame: normalise (interior 1/sum w^2),
+  // output scale, store at byte offset so of ry, chunk peak
+  auto emit_full = [&](const cf (&v)[NR], __amdgpu_buffer_rsrc_t ry, int so) {
+    float wv[SHQ];
+#pragma unroll
+    for (int q = 0; q < SHQ / 4; ++q) {
+      const float4 t = reinterpret_cast<const float4*>(s_winv)[q * P + L];
+      wv[4 * q] = t.x;
+      wv[4 * q + 1] = t.y;
+      wv[4 * q + 2] = t.z;
+      wv[4 * q + 3] = t.w;
+    }
+#pragma unroll
+    for (int i = 0; i < SH; ++i) {
+      const cf o = cscale(cscale(v[i], wv[i]), oscale);
+      if constexpr (NT) bstore<CH, 2>(o, ry, L * CH * 4, so + P * i * CH * 4);
+      else bstore<CH>(o, ry, L * CH * 4, so + P * i * CH * 4);
+      pk = fmaxf(pk, cmag<CH>(o));
     }
   };
-  cf nx[NR];
-  if constexpr (PF) load_frame(kfirst, nx);
 
-  for (int it = 0; it < nit; ++it) {
-    const int64_t k = kfirst + it;
-    const bool live = valid && (k < R.kb);
-    const int64_t s_k = S.first_start + k * HOP;
-    const uint16_t row = live ? A.rows[S.frame_base + k] : 0;
-    cf v[NR];
-    if constexpr (PF) {
+  bool fast_run = false;
+  if constexpr (P == 64) fast_run = valid && (R.last & kRunInterior);
+  if (fast_run) {
+    // Interior run (host-marked): every frame of [kfirst, kb) reads a full frame
+    // and every emitted hop block is a full interior block (no stream edges, no
+    // stream tail).  One buffer resource per run for input and for output; the
+    // hot loop carries only the frame counter, the chunk walk and the OLA.
+    const int nwarm = (int)(R.ka - kfirst);
+    const int64_t s0 = S.first_start + kfirst * HOP;
+    const __amdgpu_buffer_rsrc_t rx =
+        mk_rsrc(xs + CH * s0, (uint32_t)(((int64_t)(nit - 1) * HOP + N) * CH * 4));
+    const __amdgpu_buffer_rsrc_t ry =
+        mk_rsrc(ys + CH * (s_ka - S.out_begin), (uint32_t)((int64_t)(nit - nwarm) * HOP * CH * 4));
+    // gain-row ids through the scalar cache: the aligned 32-bit word holding the
+    // frame's u16 id, loaded one frame ahead (s_load: lgkmcnt, so waiting for it
+    // never waits for this wave's vector stores as an in-order vmcnt wait would)
+    cu32* const rw32 = (cu32*)(A.rows);
+    const int64_t fb = S.frame_base + kfirst;
+    auto row_word = [&](int it) -> uint32_t { return rw32[(fb + it) >> 1]; };
+    auto row_of = [&](uint32_t w, int it) -> uint32_t {
+      return ((fb + it) & 1) ? (w >> 16) : (w & 0xffffu);
+    };
+    // Input pipeline.  Registers 0..NO-1 of frame it+1 are registers SH.. of
+    // frame it (L2-resident): they are loaded at the end of frame it, after its
+    // transforms and before its stores.  The frame's new hop (registers NO..NR-1,
+    // from HBM) is loaded a whole frame earlier.  Every iteration issues the same
+    // vector-memory ops in the same order (clamped frame indices; warm-up frames
+    // store to a null buffer, which drops the stores), so the vmcnt wait for a
+    // frame's input never waits for the previous frame's stores or for the next
+    // new hop; and the load destinations are not live during the transforms.
+    constexpr int NO = NR - SH;
+    auto ld_old = [&](int it, cf (&dst)[NR]) {
+      const int so = it * (HOP * CH * 4);
 #pragma unroll
-      for (int n2 = 0; n2 < NR; ++n2) v[n2] = nx[n2];
-      if (it + 1 < nit) load_frame(k + 1, nx);
-    } else {
-      load_frame(k, v);
-    }
-    // ---- analysis window (x * in_scale first, two roundings as the reference) ----
-    if (iscale != 1.0f) {
-#pragma unroll
-      for (int n2 = 0; n2 < NR; ++n2) v[n2] = cscale(v[n2], iscale);
-    }
-#pragma unroll
-    for (int n4 = 0; n4 < NR / 4; ++n4) {
-      const float4 w = w4[n4 * P + L];
-      v[4 * n4] = cscale(v[4 * n4], w.x);
-      v[4 * n4 + 1] = cscale(v[4 * n4 + 1], w.y);
-      v[4 * n4 + 2] = cscale(v[4 * n4 + 2], w.z);
-      v[4 * n4 + 3] = cscale(v[4 * n4 + 3], w.w);
-    }
-    fft_fwd<P, NR>(v, L, s_twN, s_twP, buf);
-    // ---- gain row (real, even, 1/N folded in), per-lane layout ----
-    if constexpr (GLDS) {
-      const float4* g4 = reinterpret_cast<const float4*>(s_gain + (row ? N : 0));
-#pragma unroll
-      for (int n4 = 0; n4 < NR / 4; ++n4) {
-        const float4 g = g4[n4 * P + L];
-        v[4 * n4] = cscale(v[4 * n4], g.x);
-        v[4 * n4 + 1] = cscale(v[4 * n4 + 1], g.y);
-        v[4 * n4 + 2] = cscale(v[4 * n4 + 2], g.z);
-        v[4 * n4 + 3] = cscale(v[4 * n4 + 3], g.w);
+      for (int n2 = 0; n2 < NO; ++n2) {  // the frame's first hop is read for the last time (nt)
+        if (NT && n2 < SH) dst[n2] = bload<CH, 2>(rx, L * CH * 4, so + P * n2 * CH * 4);
+        else dst[n2] = bload<CH>(rx, L * CH * 4, so + P * n2 * CH * 4);
       }
-    } else {
-      const __amdgpu_buffer_rsrc_t rg = mk_rsrc(A.gains + (int64_t)row * N, N * 4);
+    };
+    auto ld_new = [&](int it, cf (&dst)[SH]) {
+      const int so = it * (HOP * CH * 4) + P * NO * CH * 4;
 #pragma unroll
-      for (int n4 = 0; n4 < NR / 4; ++n4) {
-        const f32x4 g = __builtin_amdgcn_raw_buffer_load_b128(rg, L * 16, n4 * P * 16, 0);
-        v[4 * n4] = cscale(v[4 * n4], __uint_as_float(g.x));
-        v[4 * n4 + 1] = cscale(v[4 * n4 + 1], __uint_as_float(g.y));
-        v[4 * n4 + 2] = cscale(v[4 * n4 + 2], __uint_as_float(g.z));
-        v[4 * n4 + 3] = cscale(v[4 * n4 + 3], __uint_as_float(g.w));
+      for (int j = 0; j < SH; ++j) dst[j] = bload<CH>(rx, L * CH * 4, so + P * j * CH * 4);
+    };
+    const __amdgpu_buffer_rsrc_t rnull = mk_rsrc(ys, 0u);
+    float wv[SHQ];
+    auto store_out = [&](const cf (&o)[SH], __amdgpu_buffer_rsrc_t r, int so) {
+#pragma unroll
+      for (int i = 0; i < SH; ++i) {
+        if constexpr (NT) bstore<CH, 2>(o[i], r, L * CH * 4, so + P * i * CH * 4);
+        else bstore<CH>(o[i], r, L * CH * 4, so + P * i * CH * 4);
       }
-    }
-    fft_inv<P, NR>(v, L, s_twN, s_twP, buf);
-    // ---- synthesis window fused with the register OLA ----
+    };
+    cf v[NR], nh[SH], o[SH];
+    uint32_t rw_nx = row_word(0);
+    {  // frame 0, null stores (the loop's issue pattern), new hop of frame 1
+      ld_old(0, v);
+      cf t[SH];
+      ld_new(0, t);
 #pragma unroll
-    for (int n4 = 0; n4 < NR / 4; ++n4) {
-      const float4 w = w4[n4 * P + L];
-      const float ww[4] = {w.x, w.y, w.z, w.w};
+      for (int j = 0; j < SH; ++j) v[NO + j] = t[j];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int i = 4 * n4 + u;
-        if (i < NC)
-          v[i] = {__builtin_fmaf(v[i].x, ww[u], acc[i].x), __builtin_fmaf(v[i].y, ww[u], acc[i].y)};
-        else
-          v[i] = cscale(v[i], ww[u]);
-      }
+      for (int i = 0; i < SH; ++i) o[i] = cf{0.f, 0.f};
+      store_out(o, rnull, 0);
+      ld_new(min(1, nit - 1), nh);
     }
-    if (live && k >= R.ka) {
-      if (k == next_chunk_k) {
+    for (int it = 0; it < nit; ++it) {
+      const uint32_t row = row_of(rw_nx, it);
+      rw_nx = row_word(min(it + 1, nit - 1));
+      TPROF(0, v[0].x);
+      transform(v, row);
+      TPROF(5, v[NR - 1].x);
+      const bool emit = it >= nwarm;
+      if (emit && kfirst + it == next_chunk_k) {
         flush_peak<P>(pk, cid, S, A.peaks, L, done);
         ++cid;
         next_chunk_k = (cid < S.n_chunks - 1) ? next_chunk_k + chunk_k_step : INT64_MAX;
       }
-      const bool full = (s_k >= S.out_begin) && (s_k + HOP <= out_end);
-      const bool edge = (k < A.rmax - 1);
-      if (full && !edge) {
-        const __amdgpu_buffer_rsrc_t ry = mk_rsrc(ys + CH * (s_k - S.out_begin), HOP * CH * 4);
-        float wv[SHQ];
+      // outputs of this frame's first hop: interior 1/sum w^2, output scale, peak
 #pragma unroll
-        for (int q = 0; q < SHQ / 4; ++q) {
-          const float4 t = reinterpret_cast<const float4*>(s_winv)[q * P + L];
-          wv[4 * q] = t.x;
-          wv[4 * q + 1] = t.y;
-          wv[4 * q + 2] = t.z;
-          wv[4 * q + 3] = t.w;
-        }
+      for (int q = 0; q < SHQ / 4; ++q) {
+        const float4 t4 = reinterpret_cast<const float4*>(s_winv)[q * P + L];
+        wv[4 * q] = t4.x;
+        wv[4 * q + 1] = t4.y;
+        wv[4 * q + 2] = t4.z;
+        wv[4 * q + 3] = t4.w;
+      }
+      float pf = 0.f;
 #pragma unroll
-        for (int i = 0; i < SH; ++i) {
-          const cf o = cscale(cscale(v[i], wv[i]), oscale);
-          if constexpr (NT) bstore<CH, 2>(o, ry, L * CH * 4, P * i * CH * 4);
-          else bstore<CH>(o, ry, L * CH * 4, P * i * CH * 4);
-          pk = fmaxf(pk, cmag<CH>(o));
+      for (int i = 0; i < SH; ++i) {
+        o[i] = cscale(cscale(v[i], wv[i]), oscale);
+        pf = fmaxf(pf, cmag<CH>(o[i]));
+      }
+      if (emit) pk = fmaxf(pk, pf);
+#pragma unroll
+      for (int i = 0; i < NC; ++i) acc[i] = v[i + SH];
+      // next frame's input (clamped), then this frame's stores, then the new hop
+      // of the frame after next
+#if defined(TM_EXP_L1LOAD)  // timing experiments: inputs from one L1-resident frame
+      ld_old(0, v);
+#else
+      ld_old(min(it + 1, nit - 1), v);
+#endif
+#pragma unroll
+      for (int j = 0; j < SH; ++j) v[NO + j] = nh[j];
+#if defined(TM_EXP_NOSTORE)  // timing experiments: outputs dropped
+      store_out(o, rnull, 0);
+#else
+      store_out(o, emit ? ry : rnull, emit ? (it - nwarm) * (HOP * CH * 4) : 0);
+#endif
+#if defined(TM_EXP_L1LOAD)
+      ld_new(0, nh);
+#else
+      ld_new(min(it + 2, nit - 1), nh);
+#endif
+      TPROF(6, acc[0].x);
+    }
+#ifdef TM_PROFILE
+    if (L == 0) {
+      for (int i = 0; i < 7; ++i) atomicAdd(A.prof + i, tacc[i]);
+      atomicAdd(A.prof + 15, (unsigned long long)nit);
+    }
+#endif
+  } else {
+#ifndef TM_DEV_NO_GENERIC  // timing experiments only: interior loop alone
+    // frame loads are software-pipelined one frame ahead (the next frame's HBM/L2
+    // latency hides behind this frame's transforms)
+    auto load_frame = [&](int64_t kk, cf (&dst)[NR]) {
+      const bool lv = valid && (kk < R.kb);
+      const int64_t sk = S.first_start + kk * HOP;
+      if (lv && sk >= 0 && sk + N <= S.n) {
+        const __amdgpu_buffer_rsrc_t rx = mk_rsrc(xs + CH * sk, N * CH * 4);
+  #pragma unroll
+        for (int n2 = 0; n2 < NR; ++n2) {
+          // the frame's first hop is read for the last time: stream it (nt)
+          if (NT && n2 < SH) dst[n2] = bload<CH, 2>(rx, L * CH * 4, P * n2 * CH * 4);
+          else dst[n2] = bload<CH>(rx, L * CH * 4, P * n2 * CH * 4);
         }
       } else {
-#pragma unroll
-        for (int i = 0; i < SH; ++i) {
-          const int64_t p = s_k + L + P * i;
-          if (p >= S.out_begin && p < out_end) {
-            const float d = norm_den(wsum_rel(p - S.first_start, S.n_frames, HOP, N, A.win2),
-                                     A.norm_mode);
-            const cf o = cscale(cf{v[i].x / d, v[i].y / d}, oscale);
-            store_cf<CH>(ys, p - S.out_begin, o);
-            pk = fmaxf(pk, cmag<CH>(o));
+        const int Lo = opaque(L);
+  #pragma unroll
+        for (int n2 = 0; n2 < NR; ++n2) {
+          const int64_t p = sk + Lo + P * n2;
+          dst[n2] = (lv && p >= 0 && p < S.n) ? load_cf<CH>(xs, p) : cf{0.f, 0.f};
+        }
+      }
+    };
+    // gain-row id of a frame: an unconditional load at a clamped index, issued one
+    // frame ahead at the top of the previous frame, i.e. before that frame's
+    // output stores, so the in-order vmcnt wait for it does not wait for them.
+    const int64_t kmax = valid ? R.kb - 1 : 0;
+    auto load_row = [&](int64_t kk) -> uint32_t {
+      return A.rows[S.frame_base + min(kk, kmax)];
+    };
+    cf nx[NR];
+    uint32_t row_nx = load_row(kfirst);
+    if constexpr (PF) load_frame(kfirst, nx);
+
+    for (int it = 0; it < nit; ++it) {
+      const int64_t k = kfirst + it;
+      const bool live = valid && (k < R.kb);
+      const int64_t s_k = S.first_start + k * HOP;
+      const uint32_t row = __builtin_amdgcn_readfirstlane(live ? row_nx : 0u);
+      row_nx = load_row(k + 1);
+      cf v[NR];
+      if constexpr (PF) {
+  #pragma unroll
+        for (int n2 = 0; n2 < NR; ++n2) v[n2] = nx[n2];
+        if (it + 1 < nit) load_frame(k + 1, nx);
+      } else {
+        load_frame(k, v);
+      }
+      transform(v, row);
+      if (live && k >= R.ka) {
+        if (k == next_chunk_k) {
+          flush_peak<P>(pk, cid, S, A.peaks, L, done);
+          ++cid;
+          next_chunk_k = (cid < S.n_chunks - 1) ? next_chunk_k + chunk_k_step : INT64_MAX;
+        }
+        const bool full = (s_k >= S.out_begin) && (s_k + HOP <= out_end);
+        const bool edge = (k < A.rmax - 1);
+        if (full && !edge) {
+          emit_full(v, mk_rsrc(ys + CH * (s_k - S.out_begin), HOP * CH * 4), 0);
+        } else {
+          const int Lo = opaque(L);
+  #pragma unroll
+          for (int i = 0; i < SH; ++i) {
+            const int64_t p = s_k + Lo + P * i;
+            if (p >= S.out_begin && p < out_end) {
+              const float d = norm_den(wsum_rel(p - S.first_start, S.n_frames, HOP, N, A.win2),
+                                       A.norm_mode);
+              const cf o = cscale(cf{v[i].x / d, v[i].y / d}, oscale);
+              store_cf<CH>(ys, p - S.out_begin, o);
+              pk = fmaxf(pk, cmag<CH>(o));
+            }
+          }
+        }
+        if ((R.last & 1) && k == R.kb - 1) {  // stream tail after the last frame
+          const int Lo = opaque(L);
+  #pragma unroll
+          for (int i = SH; i < NR; ++i) {
+            const int64_t p = s_k + Lo + P * i;
+            if (p >= S.out_begin && p < out_end) {
+              const float d = norm_den(wsum_rel(p - S.first_start, S.n_frames, HOP, N, A.win2),
+                                       A.norm_mode);
+              const cf o = cscale(cf{v[i].x / d, v[i].y / d}, oscale);
+              store_cf<CH>(ys, p - S.out_begin, o);
+              pk = fmaxf(pk, cmag<CH>(o));
+            }
           }
         }
       }
-      if (R.last && k == R.kb - 1) {  // stream tail after the last frame
-#pragma unroll
-        for (int i = SH; i < NR; ++i) {
-          const int64_t p = s_k + L + P * i;
-          if (p >= S.out_begin && p < out_end) {
-            const float d = norm_den(wsum_rel(p - S.first_start, S.n_frames, HOP, N, A.win2),
-                                     A.norm_mode);
-            const cf o = cscale(cf{v[i].x / d, v[i].y / d}, oscale);
-            store_cf<CH>(ys, p - S.out_begin, o);
-            pk = fmaxf(pk, cmag<CH>(o));
-          }
-        }
-      }
+  #pragma unroll
+      for (int i = 0; i < NC; ++i) acc[i] = v[i + SH];
     }
-#pragma unroll
-    for (int i = 0; i < NC; ++i) acc[i] = v[i + SH];
+#endif
   }
   if (valid) flush_peak<P>(pk, cid, S, A.peaks, L, done);
   if (valid && done) {
     // this wave's own output range (stores of frames [ka, kb) and the stream tail)
     const int64_t s_last = S.first_start + (R.kb - 1) * HOP;
     const int64_t lo = max(s_ka, S.out_begin) - S.out_begin;
-    const int64_t hi = min(s_last + (R.last ? (int64_t)N : (int64_t)HOP), out_end) - S.out_begin;
+    const int64_t hi = min(s_last + ((R.last & 1) ? (int64_t)N : (int64_t)HOP), out_end) - S.out_begin;
     // P > 64: both waves of the sequence cover the same range; split it by wave
     const int nw = P / 64, w = L >> 6;
     const int64_t span = hi - lo, per = (span + nw - 1) / nw;
@@ -395,6 +581,16 @@ __global__ __launch_bounds__(256, 2) void k_stft_ola(MainArgs A) {
     for (int c = cid_first; c <= cid; ++c)
       limit_own<CH>(A, S, S.chunk_base + c, wlo, whi, L & 63);
   }
+#ifdef TM_PROFILE
+  if (valid && (R.last & kRunInterior) && L == 0) {
+    const unsigned long long t_k2 = __builtin_amdgcn_s_memtime();
+    const unsigned long long rt_k2 = __builtin_amdgcn_s_memrealtime();
+    atomicAdd(A.prof + 7, t_k1 - t_k0);    // prologue (tables -> LDS)
+    atomicAdd(A.prof + 8, t_k2 - t_k0);    // wave lifetime
+    atomicAdd(A.prof + 9, rt_k2 - rt_k0);  // lifetime in 100 MHz ticks
+    atomicAdd(A.prof + 10, 1ull);          // waves
+  }
+#endif
 }
 
 // Generic hop: same transform, windowed frame outputs to scratch, then a gather.
@@ -517,46 +713,89 @@ __global__ __launch_bounds__(256) void k_ola_gather(MainArgs A, int n_streams,
 }
 
 
-template <int P, int NR, int SH, bool PF, bool NT>
-void launch_main_pf(const MainArgs& A, int ch, int nseq_blocks, hipStream_t s) {
+template <int P, int NR, int SH, bool PF, bool NT, int WG>
+void launch_main_pf(const MainArgs& A, int ch, hipStream_t s) {
   const bool gl = A.n_rows_lds > 0;
+  const dim3 g((A.n_runs + WG / P - 1) / (WG / P)), b(WG);
+#ifdef TM_DEV_ONE_KERNEL  // asm studies: one instantiation (stereo, LDS gains, WG 256)
+  if constexpr (WG == 256) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, true, PF, NT, WG>), g, b, 0, s, A);
+  return;
+#endif
   if (ch == 2) {
-    if (gl) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, true, PF, NT>), dim3(nseq_blocks), dim3(256), 0, s, A);
-    else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, false, PF, NT>), dim3(nseq_blocks), dim3(256), 0, s, A);
+    if (gl) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, true, PF, NT, WG>), g, b, 0, s, A);
+    else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, false, PF, NT, WG>), g, b, 0, s, A);
   } else {
-    if (gl) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, true, PF, NT>), dim3(nseq_blocks), dim3(256), 0, s, A);
-    else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, false, PF, NT>), dim3(nseq_blocks), dim3(256), 0, s, A);
+    if (gl) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, true, PF, NT, WG>), g, b, 0, s, A);
+    else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, false, PF, NT, WG>), g, b, 0, s, A);
   }
 }
 template <int P, int NR, int SH>
-void launch_main(const MainArgs& A, int ch, int nseq_blocks, hipStream_t s) {
+void launch_main(const MainArgs& A, int ch, int wg, hipStream_t s) {
   // frame prefetch pays for NR = 16 (2 waves/SIMD kept); NR = 32 is register-bound.
   // Streaming (nt) hints on last-use input and on output keep the frame overlap
   // resident in L2 (FETCH_SIZE 4.5 -> 1.8 GB per C2 launch at P = 64).
-  launch_main_pf<P, NR, SH, NR == 16, true>(A, ch, nseq_blocks, s);
+  // Workgroup size: the LDS tables (twiddles, window, gain rows) are per block,
+  // so wider blocks share them among more sequences and lift the LDS-bound
+  // occupancy (see transform_wg).
+  // P = 64: the interior loop pipelines its own input; PF only affects the
+  // generic edge loop, where it stays off (register-bound).
+  constexpr bool PF = NR == 16;
+  if constexpr (P == 64) {
+    if (wg == 512) return launch_main_pf<P, NR, SH, false, true, 512>(A, ch, s);
+    return launch_main_pf<P, NR, SH, false, true, 256>(A, ch, s);
+  }
+  if constexpr (P == 128 && NR == 32) {
+    if (wg == 512) return launch_main_pf<P, NR, SH, PF, true, 512>(A, ch, s);
+  }
+  launch_main_pf<P, NR, SH, PF, true, 256>(A, ch, s);
 }
 
 }  // namespace
 
 namespace tshared {
 
-void launch_transform(const MainArgs& A, int P, int NR, int SH, int ch, int blocks, hipStream_t s) {
+int transform_wg(int P, int NR) {
+  // P = 64 (n_fft 2048): the interior loop needs ~250 VGPRs (2 waves/SIMD), so
+  // two 4-sequence blocks per CU (TOMATIS_WG=512: one 8-sequence block, the
+  // same occupancy with one copy of the tables; measured equal).
+  // P = 128, NR = 32 (n_fft 4096): 4 two-wave sequences (~120 KB, 2 waves/SIMD).
+  const int dflt = P == 64 ? 256 : (NR == 32 ? 512 : 256);
+  const int w = env_int("TOMATIS_WG", dflt);
+  if (P == 64 && (w == 256 || w == 512)) return w;
+  if (P == 128 && NR == 32 && (w == 256 || w == 512)) return w;
+  return P == 128 && NR == 16 ? 256 : dflt;
+}
+
+int transform_slots_per_cu(int P, int NR) {
+  // resident sequences per CU: 256-thread blocks run two per CU, wider ones one
+  const int wg = transform_wg(P, NR);
+  return (wg == 256 ? 2 : 1) * (wg / P);
+}
+
+void launch_transform(const MainArgs& A, int P, int NR, int SH, int ch, int wg, hipStream_t s) {
+#ifdef TM_DEV_ONLY_2048_512  // development builds: the headline configuration only
+  if (P == 64 && SH == 8) launch_main<64, 32, 8>(A, ch, wg, s);
+  return;
+#endif
   if (P == 64) {
-    if (SH == 4) launch_main<64, 32, 4>(A, ch, blocks, s);
-    else if (SH == 8) launch_main<64, 32, 8>(A, ch, blocks, s);
-    else launch_main<64, 32, 16>(A, ch, blocks, s);
+    if (SH == 4) launch_main<64, 32, 4>(A, ch, wg, s);
+    else if (SH == 8) launch_main<64, 32, 8>(A, ch, wg, s);
+    else launch_main<64, 32, 16>(A, ch, wg, s);
   } else if (NR == 16) {
-    if (SH == 2) launch_main<128, 16, 2>(A, ch, blocks, s);
-    else if (SH == 4) launch_main<128, 16, 4>(A, ch, blocks, s);
-    else launch_main<128, 16, 8>(A, ch, blocks, s);
+    if (SH == 2) launch_main<128, 16, 2>(A, ch, wg, s);
+    else if (SH == 4) launch_main<128, 16, 4>(A, ch, wg, s);
+    else launch_main<128, 16, 8>(A, ch, wg, s);
   } else {
-    if (SH == 4) launch_main<128, 32, 4>(A, ch, blocks, s);
-    else if (SH == 8) launch_main<128, 32, 8>(A, ch, blocks, s);
-    else launch_main<128, 32, 16>(A, ch, blocks, s);
+    if (SH == 4) launch_main<128, 32, 4>(A, ch, wg, s);
+    else if (SH == 8) launch_main<128, 32, 8>(A, ch, wg, s);
+    else launch_main<128, 32, 16>(A, ch, wg, s);
   }
 }
 
 void launch_frames(const MainArgs& A, int P, int NR, int blocks, hipStream_t s) {
+#ifdef TM_DEV_ONE_KERNEL
+  return;
+#endif
   if (P == 64) hipLaunchKernelGGL((k_stft_frames<64, 32>), dim3(blocks), dim3(256), 0, s, A);
   else if (NR == 16) hipLaunchKernelGGL((k_stft_frames<128, 16>), dim3(blocks), dim3(256), 0, s, A);
   else hipLaunchKernelGGL((k_stft_frames<128, 32>), dim3(blocks), dim3(256), 0, s, A);

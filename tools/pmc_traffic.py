@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Write profiles/pmc_traffic.json from rocprofv3 FETCH_SIZE / WRITE_SIZE passes.
+
+Usage: tools/pmc_traffic.py PMC_DIR WORKLOAD [--kernel k_stft_ola] [--alg-bytes B]
+
+PMC_DIR holds the per-pass rocprofv3 outputs of tools/pmc.sh or
+tools/pmc_fetch.sh (p*/run_counter_collection.csv).  For the fused kernel the
+per-dispatch counters are averaged over its dispatches and converted to bytes
+the way MI355X_MICROARCH.md (HBM / rocprofv3 section) prescribes:
+FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the
+bytes of a wide coalesced streaming read, so reads = 2 x FETCH_SIZE.  The
+kernel's input loads are 8-byte-per-lane buffer loads, a width the guide lists
+as uncalibrated, so the uncorrected figure is kept beside the corrected one.
+bench.py reads "hbm_bytes_per_launch" for its roofline.traffic field.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def main():
+    a = sys.argv[1:]
+    d, workload = a[0], a[1]
+    kern = a[a.index("--kernel") + 1] if "--kernel" in a else "k_stft_ola"
+    alg = float(a[a.index("--alg-bytes") + 1]) if "--alg-bytes" in a else None
+    vals = defaultdict(list)
+    for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
+        for r in csv.DictReader(open(f)):
+            if kern in r["Kernel_Name"]:
+                vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    if "FETCH_SIZE" not in vals or "WRITE_SIZE" not in vals:
+        sys.exit(f"no FETCH_SIZE/WRITE_SIZE dispatches of {kern} under {d}")
+    fetch_kib = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"])
+    write_kib = sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"])
+    rd = 2.0 * fetch_kib * 1024.0
+    wr = write_kib * 1024.0
+    out_path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "profiles", "pmc_traffic.json")
+    try:
+        doc = json.load(open(out_path))
+    except (OSError, ValueError):
+        doc = {}
+    rec = {"kernel": kern, "dispatches": len(vals["FETCH_SIZE"]),
+           "fetch_size_kib": fetch_kib, "write_size_kib": write_kib,
+           "read_bytes_corrected": rd, "write_bytes": wr,
+           "hbm_bytes_per_launch": rd + wr,
+           "hbm_bytes_uncorrected": fetch_kib * 1024.0 + wr,
+           "source": os.path.relpath(d),
+           "correction": "reads = 2 x FETCH_SIZE (gfx950, MI355X_MICROARCH.md HBM section)"}
+    if alg:
+        rec["alg_bytes_per_launch"] = alg
+        rec["traffic_over_alg"] = (rd + wr) / alg
+    doc[workload] = rec
+    with open(out_path, "w") as f:
+        json.dump(doc, f, indent=1)
+    print(json.dumps(rec, indent=1))
+
+
+if __name__ == "__main__":
+    main()
