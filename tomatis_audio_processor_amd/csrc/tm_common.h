@@ -62,8 +62,20 @@ constexpr double ct_sin2pi(long m, long M) { return ct_cos2pi(m - M / 4, M); }  
 struct cf {
   float x, y;
 };
+#ifdef TM_PACKED  // complex add/sub as one v_pk_add_f32 (gfx950 packed fp32)
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ cf operator+(cf a, cf b) {
+  const f2v r = f2v{a.x, a.y} + f2v{b.x, b.y};
+  return {r.x, r.y};
+}
+__device__ __forceinline__ cf operator-(cf a, cf b) {
+  const f2v r = f2v{a.x, a.y} - f2v{b.x, b.y};
+  return {r.x, r.y};
+}
+#else
 __device__ __forceinline__ cf operator+(cf a, cf b) { return {a.x + b.x, a.y + b.y}; }
 __device__ __forceinline__ cf operator-(cf a, cf b) { return {a.x - b.x, a.y - b.y}; }
+#endif
 __device__ __forceinline__ cf cmul(cf a, cf w) {  // a * w
   return {__builtin_fmaf(a.x, w.x, -(a.y * w.y)), __builtin_fmaf(a.x, w.y, a.y * w.x)};
 }

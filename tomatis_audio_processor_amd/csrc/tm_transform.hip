@@ -747,6 +747,10 @@ void launch_main(const MainArgs& A, int ch, int wg, hipStream_t s) {
   if constexpr (P == 128 && NR == 32) {
     if (wg == 512) return launch_main_pf<P, NR, SH, PF, true, 512>(A, ch, s);
   }
+  if constexpr (P == 128 && NR == 16) {  // 114 VGPRs: 3 waves/SIMD at 768 threads
+    if (wg == 768) return launch_main_pf<P, NR, SH, PF, true, 768>(A, ch, s);
+    if (wg == 512) return launch_main_pf<P, NR, SH, PF, true, 512>(A, ch, s);
+  }
   launch_main_pf<P, NR, SH, PF, true, 256>(A, ch, s);
 }
 
@@ -763,7 +767,8 @@ int transform_wg(int P, int NR) {
   const int w = env_int("TOMATIS_WG", dflt);
   if (P == 64 && (w == 256 || w == 512)) return w;
   if (P == 128 && NR == 32 && (w == 256 || w == 512)) return w;
-  return P == 128 && NR == 16 ? 256 : dflt;
+  if (P == 128 && NR == 16 && (w == 256 || w == 512 || w == 768)) return w;
+  return dflt;
 }
 
 int transform_slots_per_cu(int P, int NR) {
