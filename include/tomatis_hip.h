@@ -150,7 +150,10 @@ int tomatis_minhold_bisect(tomatis_plan_t plan, const double* levels,
 
 /* Fused framing -> window -> FFT -> gain row -> IFFT -> window -> OLA ->
  * normalise -> out_scale, plus per-chunk |y| maxima as float bits
- * (chunk_peak_bits must be zeroed by the caller; uint32 per chunk). */
+ * (chunk_peak_bits must be zeroed by the caller; uint32 per chunk).
+ * rows: one uint16 gain-row id per frame; the kernel reads it through the
+ * scalar cache in aligned 4-byte words, so the allocation must cover
+ * total_frames rounded up to an even count. */
 int tomatis_stft_ola(tomatis_plan_t plan, const float* x, const float* gain_rows,
                      int32_t n_rows, const uint16_t* rows, float* y,
                      uint32_t* chunk_peak_bits, void* hip_stream);

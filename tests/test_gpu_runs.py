@@ -1,0 +1,83 @@
+"""GPU: the fused kernel's work decomposition does not change a single bit.
+
+The host cuts every stream into interior runs (fast loop) and edge runs
+(generic loop) and sizes runs to the device's resident slots
+(tm_kernels.hip plan_build); the limiter is fused in-kernel or run as a second
+launch.  Every output hop block is the same frame-ordered float32 sum whatever
+the cut, so outputs, chunk peaks and states must be bitwise identical across:
+run lengths (TOMATIS_RUN_FRAMES), the interior loop on/off (TOMATIS_FAST_LOOP),
+and the fused/unfused limiter (TOMATIS_FUSE_LIMITER).  One small case is also
+checked against the oracle.  Streams of unequal, odd lengths make frame_base
+odd for some streams (the gain-row ids are read as aligned 32-bit words).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import tomatis_oracle as orc
+from tomatis_audio_processor_amd.synth import synth_stream
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from tomatis_audio_processor_amd import engine
+    return torch, engine
+
+
+def _run(E, torch, xs, sr, env, **params):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        ss = E.StreamSet.from_arrays(xs, sr)
+        pipe = E.GatePipeline(ss, **params)
+        res = pipe.run()
+        torch.cuda.synchronize()
+        pipe.plan.check_device()
+        outs = [res.output(i) for i in range(len(xs))]
+        sts = [res.stream_states(i) for i in range(len(xs))]
+        pks = [res.stream_peaks(i) for i in range(len(xs))]
+        return outs, sts, pks
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("n_fft,hop,sr", [(2048, 512, 44100), (4096, 1024, 96000),
+                                          (4096, 2048, 48000)])
+def test_decomposition_bit_identical(n_fft, hop, sr):
+    torch, E = _engine()
+    lens = [sr * 37 + 1, sr * 20 + 259, sr * 61 + 777]  # odd frame counts -> odd frame_base
+    xs = [synth_stream(500 + i, n, 2, sr) for i, n in enumerate(lens)]
+    params = dict(gate_ui=50, n_fft=n_fft, hop=hop)
+    base = _run(E, torch, xs, sr, {}, **params)
+    variants = [{"TOMATIS_RUN_FRAMES": 48}, {"TOMATIS_RUN_FRAMES": 131},
+                {"TOMATIS_RUN_FRAMES": 1000}, {"TOMATIS_FAST_LOOP": 0},
+                {"TOMATIS_FUSE_LIMITER": 0}, {"TOMATIS_RUN_FRAMES": 77, "TOMATIS_FUSE_LIMITER": 0}]
+    for env in variants:
+        got = _run(E, torch, xs, sr, env, **params)
+        for i in range(len(xs)):
+            assert np.array_equal(got[1][i], base[1][i]), (env, i, "states")
+            assert got[2][i].tobytes() == base[2][i].tobytes(), (env, i, "chunk peaks")
+            assert got[0][i].tobytes() == base[0][i].tobytes(), (env, i, "samples")
+
+
+def test_small_runs_vs_oracle():
+    """Many interior/edge run boundaries (48-frame runs) against the oracle."""
+    torch, E = _engine()
+    sr, N = 48000, 48000 * 12 + 333
+    x = synth_stream(9, N, 2, sr)
+    outs, sts, _ = _run(E, torch, [x], sr, {"TOMATIS_RUN_FRAMES": 48},
+                        gate_ui=50, n_fft=2048, hop=512)
+    ref = orc.process_standard(x, sr, gate_ui=50, n_fft=2048, hop=512)
+    assert np.array_equal(sts[0], ref["states"])
+    m = ref["wsum"][ref["pad"]:ref["pad"] + N] >= 1e-3
+    err = np.abs(outs[0][m] - ref["y"][m])
+    assert float(err.max()) <= 1e-4

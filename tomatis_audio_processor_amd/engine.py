@@ -258,7 +258,7 @@ class GatePipeline:
         dev = ss.x.device
         self.r = torch.empty(Ft, dtype=torch.float32, device=dev)
         self.states = torch.empty(Ft, dtype=torch.uint8, device=dev)
-        self.rows = torch.empty(Ft, dtype=torch.int16, device=dev)
+        self.rows = torch.empty(Ft + 1, dtype=torch.int16, device=dev)  # +1: read as u32 words
         self.alpha = torch.empty(Ft, dtype=torch.float64, device=dev) if self.xfade else None
         self.peaks = torch.zeros(max(1, self.plan.total_chunks), dtype=torch.int32, device=dev)
         self.gains = torch.from_numpy(np.stack(rows).astype(np.float32)).to(dev)
@@ -363,7 +363,7 @@ class AdaptivePipeline:
         self.r64 = torch.empty(Ft, dtype=torch.float64, device=dev)
         self.levels = torch.empty(Ft, dtype=torch.float64, device=dev)
         self.states = torch.empty(Ft, dtype=torch.uint8, device=dev)
-        self.rows = torch.empty(Ft, dtype=torch.int16, device=dev)
+        self.rows = torch.empty(Ft + 1, dtype=torch.int16, device=dev)  # +1: read as u32 words
         self.alpha = torch.empty(Ft, dtype=torch.float64, device=dev)
         self.t_out = torch.empty(max(1, ss.n_streams), dtype=torch.float64, device=dev)
         self.peaks = torch.zeros(max(1, self.plan.total_chunks), dtype=torch.int32, device=dev)
@@ -482,7 +482,7 @@ class StaticEqPipeline:
         self.plan = Plan(desc, dsp.hann(n_fft), streams)
         Ft = max(1, self.plan.total_frames)
         dev = ss.x.device
-        self.rows = torch.zeros(Ft, dtype=torch.int16, device=dev)
+        self.rows = torch.zeros(Ft + 1, dtype=torch.int16, device=dev)  # +1: read as u32 words
         self.peaks = torch.zeros(max(1, self.plan.total_chunks), dtype=torch.int32, device=dev)
         self.gains = torch.from_numpy(np.asarray(gain_bins, np.float32)[None, :].copy()).to(dev)
         self.out_offs = out_offs
