@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define TOMATIS_ABI_VERSION 2
+#define TOMATIS_ABI_VERSION 3
 
 #define TOMATIS_OK 0
 #define TOMATIS_E_ARG (-1)        /* bad argument */
@@ -137,6 +137,33 @@ int tomatis_levels(tomatis_plan_t plan, const float* x, void* r_out, int32_t pre
  * alpha = m/xfade_frames (alpha_mode 1).  alpha_out (optional, f64 per frame). */
 int tomatis_gate_std(tomatis_plan_t plan, const float* r, uint8_t* states,
                      uint16_t* rows, double* alpha_out, void* hip_stream);
+
+/* Time sharding of one stream across ranks (host side:
+ * tomatis_audio_processor_amd/timeshard.py).  The standard gate's run-scan form
+ * (plans whose thresholds admit no float32 r that is both "on" and "off",
+ * i.e. hysteresis > 0) is an associative scan over per-segment summaries:
+ *   summary (5 int32): all_on, not_on (last not-on frame), l_end (last frame
+ *     of the leading on-run), e_int (last gate entry after the first not-on
+ *     frame), off (last off frame); frame indices stream-local,
+ *     TOMATIS_GATE_NONE for none;
+ *   carry (3 int32): a (last not-on frame), e (last entry), f (last off);
+ *     C1 idle before frame 0 = (-1, NONE, NONE); state(k) = C2 iff e > f.
+ * A rank composes its predecessors' summaries into its carry-in (one
+ * all_gather of 5 ints per rank) and resolves its own frames from it.
+ * Replaces the sequential automaton src/process_tomatis.py:373-385 across a
+ * shard boundary. */
+#define TOMATIS_GATE_SEGMENT 1024          /* frames per gate segment */
+#define TOMATIS_GATE_NONE (-536870912)     /* INT_MIN / 4 */
+int32_t tomatis_plan_gate_segments(tomatis_plan_t plan);
+/* Synchronous: per-segment summaries of every stream (segments in stream order,
+ * TOMATIS_GATE_SEGMENT frames each, the last one partial), 5 int32 each, into
+ * sums_host.  TOMATIS_E_UNSUPPORTED when the gate is not in run-scan form. */
+int tomatis_gate_segment_sums(tomatis_plan_t plan, const float* r, int32_t* sums_host,
+                              void* hip_stream);
+/* tomatis_gate_std (standard gate, alpha_mode 0) starting every stream from
+ * carry_host[3*s .. 3*s+2] instead of C1 idle.  Synchronous. */
+int tomatis_gate_std_carry(tomatis_plan_t plan, const float* r, const int32_t* carry_host,
+                           uint8_t* states, uint16_t* rows, void* hip_stream);
 
 /* Adaptive: bisection for the min-hold threshold per stream
  * (find_optimal_threshold), final states, alpha and gain rows (2+m).

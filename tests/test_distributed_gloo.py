@@ -47,3 +47,49 @@ def test_gloo_manifest_gather(ws):
     assert sum(counts.values()) == 512 and abs(counts[0] - counts[1]) <= 2
     for _, _, shape, ids in out:
         assert shape == (512, 8) and ids == list(range(512))
+
+
+def _ts_worker(rank, ws, port, q):
+    """Time-shard exchanges over gloo: gate summaries (all_gather) and chunk
+    peaks (all_reduce MAX) reproduce the single-rank results."""
+    import numpy as np
+    import torch.distributed as dist
+    from tomatis_audio_processor_amd import timeshard as T
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    rng = np.random.default_rng(5)
+    pred = rng.choice([0, 1, 2], size=4096, p=[0.3, 0.5, 0.2]).astype(np.uint8)
+    pred = np.repeat(pred[:512], 8)  # runs of 8 frames
+    D = 7
+    bs = [0, 2560, 4096]
+    a, b = bs[rank], bs[rank + 1]
+    sums = T.exchange_summaries(T.gs_shift(T.summarize(pred[a:b], D), a))
+    mine = T.resolve(pred[a:b], D, T.carry_in(sums, rank, D), k0=a)
+    g = np.zeros(16, np.uint32)
+    g[rank * 6:rank * 6 + 10] = np.arange(10, dtype=np.uint32) + 100 * rank
+    gmax = T.exchange_peaks(g)
+    q.put((rank, mine.tolist(), gmax.tolist(), T.resolve(pred, D).tolist()))
+    dist.destroy_process_group()
+
+
+def test_gloo_timeshard_exchanges():
+    ws = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ts_worker, args=(r, ws, port, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=120) for _ in range(ws)])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    states = out[0][1] + out[1][1]
+    assert states == out[0][3]
+    exp = np.zeros(16, np.uint32)
+    for r in range(ws):
+        g = np.zeros(16, np.uint32)
+        g[r * 6:r * 6 + 10] = np.arange(10, dtype=np.uint32) + 100 * r
+        exp = np.maximum(exp, g)
+    assert out[0][2] == exp.tolist() == out[1][2]

@@ -14,7 +14,9 @@ import ctypes as C
 import os
 
 LIB_NAME = "libtomatis_hip.so"
-ABI_VERSION = 2  # include/tomatis_hip.h TOMATIS_ABI_VERSION
+ABI_VERSION = 3  # include/tomatis_hip.h TOMATIS_ABI_VERSION
+GATE_SEGMENT = 1024      # TOMATIS_GATE_SEGMENT
+GATE_NONE = -536870912   # TOMATIS_GATE_NONE
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 F32, F64 = 0, 1
@@ -63,6 +65,9 @@ _SIGS = {
     "tomatis_plan_update_streams": (C.c_int, [_P, C.POINTER(TomatisStream), _P]),
     "tomatis_levels": (C.c_int, [_P, _P, _P, C.c_int32, _P]),
     "tomatis_gate_std": (C.c_int, [_P, _P, _P, _P, _P, _P]),
+    "tomatis_plan_gate_segments": (C.c_int32, [_P]),
+    "tomatis_gate_segment_sums": (C.c_int, [_P, _P, _P, _P]),
+    "tomatis_gate_std_carry": (C.c_int, [_P, _P, _P, _P, _P, _P]),
     "tomatis_minhold_bisect": (C.c_int, [_P, _P, _P, C.c_double, C.c_double, _P, _P, _P,
                                          _P, _P]),
     "tomatis_stft_ola": (C.c_int, [_P, _P, _P, C.c_int32, _P, _P, _P, _P]),

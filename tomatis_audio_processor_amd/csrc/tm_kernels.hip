@@ -443,9 +443,12 @@ __global__ __launch_bounds__(256) void k_gate_sum(const float* __restrict__ r,
 __global__ __launch_bounds__(256) void k_gate_carry(const int32_t* __restrict__ seg_first,
                                                     const int32_t* __restrict__ seg_count, int D,
                                                     const GSum* __restrict__ sums,
-                                                    GCarry* __restrict__ carry) {
+                                                    GCarry* __restrict__ carry,
+                                                    const GCarry* __restrict__ carry_in) {
   const int a = seg_first[blockIdx.x], n = seg_count[blockIdx.x];
-  GCarry c{-1, kNI, kNI};  // initial C1 idle: run "restarts" just before frame 0
+  // initial C1 idle: run "restarts" just before frame 0; a time shard starts
+  // from the carry its predecessors' summaries compose to (timeshard.py)
+  GCarry c = carry_in ? carry_in[blockIdx.x] : GCarry{-1, kNI, kNI};
   for (int t0 = 0; t0 < n; t0 += 256) {
     const int i = t0 + threadIdx.x;
     const GSum v = (i < n) ? sums[a + i] : gs_identity();
@@ -790,6 +793,7 @@ struct tomatis_plan_s {
   bool gate_excl = false;
   void* gsum = nullptr;
   void* gcarry = nullptr;
+  void* gcarry_in = nullptr;  // time shards: carry-in per stream
   // streaming levels (hop % 128 == 0): per-stream 8-block groups and leaves
   bool leaf_path = false;
   int64_t n_groups = 0;
@@ -850,7 +854,7 @@ int tomatis_plan_destroy(tomatis_plan_t p) {
   void* ptrs[] = {p->st, p->runs, p->lblocks, p->segs, p->seg_first, p->seg_count, p->tf,
                   p->seg_start, p->win, p->win2, p->winv, p->twN, p->twP, p->scratch,
                   p->pos_base, p->chunks, p->mh_tf, p->mh_cnt, p->mh_off, p->gperm,
-                  p->grp_base, p->leaf_base, p->leaves, p->gsum, p->gcarry,
+                  p->grp_base, p->leaf_base, p->leaves, p->gsum, p->gcarry, p->gcarry_in,
                   p->chunk_need, p->chunk_done, p->chunk_rng, p->err};
   for (void* q : ptrs) dfree(q);
   delete p;
@@ -1347,7 +1351,8 @@ int tomatis_gate_std(tomatis_plan_t p, const float* r, uint8_t* states, uint16_t
     hipLaunchKernelGGL(k_gate_sum, dim3(p->n_segs), dim3(256), 0, s, r, p->st, p->segs, D,
                        (GSum*)p->gsum);
     hipLaunchKernelGGL(k_gate_carry, dim3(p->n_streams), dim3(256), 0, s, p->seg_first,
-                       p->seg_count, D, (const GSum*)p->gsum, (GCarry*)p->gcarry);
+                       p->seg_count, D, (const GSum*)p->gsum, (GCarry*)p->gcarry,
+                       (const GCarry*)nullptr);
     hipLaunchKernelGGL(k_gate_states, dim3(p->n_segs), dim3(256), 0, s, r, p->st, p->segs, D,
                        (const GCarry*)p->gcarry, states, xf ? nullptr : rows);
   } else {
@@ -1363,6 +1368,48 @@ int tomatis_gate_std(tomatis_plan_t p, const float* r, uint8_t* states, uint16_t
                        p->n_streams, states, p->d.xfade_frames, rows, alpha_out);
   }
   return launch_check();
+}
+
+int32_t tomatis_plan_gate_segments(tomatis_plan_t p) { return p ? p->n_segs : -1; }
+
+int tomatis_gate_segment_sums(tomatis_plan_t p, const float* r, int32_t* sums_host, void* hs) {
+  if (!p || !r || !sums_host) return TOMATIS_E_ARG;
+  if (!p->gate_excl) return TOMATIS_E_UNSUPPORTED;
+  if (p->n_segs == 0) return TOMATIS_OK;
+  hipStream_t s = (hipStream_t)hs;
+  hipLaunchKernelGGL(k_gate_sum, dim3(p->n_segs), dim3(256), 0, s, r, p->st, p->segs,
+                     p->d.up_delay_frames, (GSum*)p->gsum);
+  int rc = launch_check();
+  if (rc) return rc;
+  static_assert(sizeof(GSum) == 5 * sizeof(int32_t), "GSum layout");
+  if (hipMemcpyAsync(sums_host, p->gsum, (size_t)p->n_segs * sizeof(GSum), hipMemcpyDeviceToHost, s))
+    return TOMATIS_E_HIP;
+  return hipfail(hipStreamSynchronize(s));
+}
+
+int tomatis_gate_std_carry(tomatis_plan_t p, const float* r, const int32_t* carry_host,
+                           uint8_t* states, uint16_t* rows, void* hs) {
+  if (!p || !r || !carry_host || !states || !rows) return TOMATIS_E_ARG;
+  if (!p->gate_excl || p->d.alpha_mode != 0) return TOMATIS_E_UNSUPPORTED;
+  if (p->n_segs == 0) return TOMATIS_OK;
+  hipStream_t s = (hipStream_t)hs;
+  static_assert(sizeof(GCarry) == 3 * sizeof(int32_t), "GCarry layout");
+  if (!p->gcarry_in && hipMalloc(&p->gcarry_in, (size_t)std::max(1, p->n_streams) * sizeof(GCarry)))
+    return TOMATIS_E_NOMEM;
+  if (hipMemcpyAsync(p->gcarry_in, carry_host, (size_t)p->n_streams * sizeof(GCarry),
+                     hipMemcpyHostToDevice, s))
+    return TOMATIS_E_HIP;
+  const int D = p->d.up_delay_frames;
+  hipLaunchKernelGGL(k_gate_sum, dim3(p->n_segs), dim3(256), 0, s, r, p->st, p->segs, D,
+                     (GSum*)p->gsum);
+  hipLaunchKernelGGL(k_gate_carry, dim3(p->n_streams), dim3(256), 0, s, p->seg_first,
+                     p->seg_count, D, (const GSum*)p->gsum, (GCarry*)p->gcarry,
+                     (const GCarry*)p->gcarry_in);
+  hipLaunchKernelGGL(k_gate_states, dim3(p->n_segs), dim3(256), 0, s, r, p->st, p->segs, D,
+                     (const GCarry*)p->gcarry, states, rows);
+  int rc = launch_check();
+  if (rc) return rc;
+  return hipfail(hipStreamSynchronize(s));  // carry_host may be reused by the caller
 }
 
 int tomatis_minhold_bisect(tomatis_plan_t p, const double* levels, const double* tlh,

@@ -200,7 +200,10 @@ class GatePipeline:
                  dynamic_range=80.0, gate_scale=1.0, gate_offset=-100, hysteresis_db=3.0,
                  fc=1000.0, slope=12.0, c1_low=15.0, c1_high=-15.0, c2_low=-15.0,
                  c2_high=15.0, up_delay_ms=250.0, n_fft=4096, hop=2048,
-                 output_gain_db=0.0, xfade_ms=None):
+                 output_gain_db=0.0, xfade_ms=None, geometry=None):
+        """``geometry``: optional per-stream dicts (first_start, n_frames,
+        out_begin, out_len, chunk_first, chunk_len, n_chunks) replacing the
+        reference schedule -- a time shard of a longer stream (timeshard.py)."""
         torch = _torch()
         _check_fft(n_fft, hop, ss.ch)
         self.ss, self.n_fft, self.hop = ss, n_fft, hop
@@ -227,22 +230,33 @@ class GatePipeline:
         D = int(sr * up_delay_ms / 1000.0)
         self.up_delay_samples = D
         Dk = max(0, -(-D // hop))
+        self.up_delay_frames = Dk
         self.xf = xf
         out_scale = np.float32(10.0 ** (output_gain_db / 20.0)) if (
             output_gain_db != 0.0 and not self.xfade) else np.float32(1.0)
         streams = []
         self.bounds = []
-        for off, N in zip(ss.offs, ss.lens):
-            pad, pe, F, s0 = dsp.std_schedule(N, n_fft, hop)
-            b = dsp.std_flush_bounds(N, n_fft, hop)
-            self.bounds.append(b)
+        for i, (off, N) in enumerate(zip(ss.offs, ss.lens)):
             st = TomatisStream()
-            st.in_off, st.n, st.first_start, st.n_frames = off, N, s0, F
-            st.out_begin, st.out_len = 0, (N if F else 0)
-            nch = max(1, len(b) - 1)
-            st.n_chunks = nch
-            st.chunk_first = b[1] if len(b) > 2 else 0
-            st.chunk_len = (b[2] - b[1]) if len(b) > 3 else max(1, (b[-1] - b[1]) if len(b) > 2 else 1)
+            if geometry is not None:
+                g = geometry[i]
+                st.in_off, st.n = off, N
+                st.first_start, st.n_frames = g["first_start"], g["n_frames"]
+                st.out_begin, st.out_len = g["out_begin"], g["out_len"]
+                st.n_chunks, st.chunk_first, st.chunk_len = (g["n_chunks"], g["chunk_first"],
+                                                             g["chunk_len"])
+                self.bounds.append(g.get("bounds"))
+            else:
+                pad, pe, F, s0 = dsp.std_schedule(N, n_fft, hop)
+                b = dsp.std_flush_bounds(N, n_fft, hop)
+                self.bounds.append(b)
+                st.in_off, st.n, st.first_start, st.n_frames = off, N, s0, F
+                st.out_begin, st.out_len = 0, (N if F else 0)
+                nch = max(1, len(b) - 1)
+                st.n_chunks = nch
+                st.chunk_first = b[1] if len(b) > 2 else 0
+                st.chunk_len = ((b[2] - b[1]) if len(b) > 3 else
+                                max(1, (b[-1] - b[1]) if len(b) > 2 else 1))
             st.in_scale, st.out_scale = 1.0, float(out_scale)
             _set_gate(st, self.Ton, self.Toff)
             streams.append(st)

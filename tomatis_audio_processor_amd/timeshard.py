@@ -1,0 +1,339 @@
+"""Time sharding of one long stream across ranks.
+
+A 60-min stream (config C2) is one unit of the file-parallel path, so on N GPUs
+it would run on one of them.  Here its frames are cut into N contiguous shards,
+one per rank (one process per GPU), each computed by the same kernels as a
+whole stream, with two small exchanges:
+
+* **gate carry** — the standard gate (src/process_tomatis.py:373-385) is
+  sequential, but in its run-scan form it is an associative scan over
+  per-segment summaries (include/tomatis_hip.h, "Time sharding").  Each rank
+  reduces the summaries of its own frames to 5 int32, one ``all_gather``
+  collects them, and every rank composes its predecessors' into its carry-in.
+* **limiter peaks** — the 0.999 limiter's chunks (src/process_tomatis.py:
+  331-357) are global; a chunk may straddle shards, so each rank's chunk
+  maxima go through one ``all_reduce(MAX)`` before the fix-up scale.
+
+The input needs no exchange: a rank reads its slice of the stream plus a halo
+of ``rmax - 1`` warm-up frames (``n_fft - hop`` samples) before it, recomputes
+those frames (they are the previous rank's last frames) and emits only its own
+hop blocks.  Shard boundaries are placed so that every rank's summary range is
+a whole number of gate segments.  Every output sample is the same frame-ordered
+float32 sum as in the unsharded run, so the concatenated shards are
+bit-identical to it (tests/test_gpu_timeshard.py).
+
+Standard mode only (the xfade alpha and the adaptive bisection are further
+sequential scans; not sharded).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Sequence
+
+import numpy as np
+
+from . import dsp
+from ._lib import GATE_NONE as NONE, GATE_SEGMENT
+
+C1_IDLE = (-1, NONE, NONE)
+
+
+# ---------------------------------------------------------------------------
+# run-scan algebra (host mirror of tm_kernels.hip gs_cat / gs_apply)
+# ---------------------------------------------------------------------------
+
+def gs_identity():
+    return (1, NONE, NONE, NONE, NONE)
+
+
+def gs_cat(X, Y, D: int):
+    """Summary of X followed by Y (associative)."""
+    all_on = X[0] & Y[0]
+    not_on = max(X[1], Y[1])
+    off = max(X[4], Y[4])
+    if X[0]:
+        l_end = Y[2] if Y[2] != NONE else X[2]
+        e_int = Y[3]
+    else:
+        l_end = X[2]
+        lead = Y[2] if (Y[2] != NONE and Y[2] >= X[1] + D + 1) else NONE
+        e_int = max(X[3], Y[3], lead)
+    return (all_on, not_on, l_end, e_int, off)
+
+
+def gs_apply(c, S, D: int):
+    """Carry after a segment with summary S, from carry c = (a, e, f)."""
+    a = c[0] if S[0] else S[1]
+    lead = S[2] if (S[2] != NONE and S[2] >= c[0] + D + 1) else NONE
+    return (a, max(c[1], S[3], lead), max(c[2], S[4]))
+
+
+def _shift(v, off: int):
+    return v if v == NONE else v + off
+
+
+def gs_shift(S, off: int):
+    """Re-index a summary by +off frames."""
+    return (S[0], _shift(S[1], off), _shift(S[2], off), _shift(S[3], off), _shift(S[4], off))
+
+
+def carry_shift(c, off: int):
+    return (c[0] + off, _shift(c[1], off), _shift(c[2], off))
+
+
+def summarize(pred: Sequence[int], D: int, k0: int = 0):
+    """Summary of frames k0.. (host reference of k_gate_sum)."""
+    S = gs_identity()
+    for i, p in enumerate(pred):
+        k = k0 + i
+        fr = (1, NONE, k, NONE, NONE) if (p & 1) else (0, k, NONE, NONE, k if (p & 2) else NONE)
+        S = gs_cat(S, fr, D)
+    return S
+
+
+def resolve(pred: Sequence[int], D: int, carry=C1_IDLE, k0: int = 0) -> np.ndarray:
+    """States (1 = C1, 2 = C2) of frames k0.. from a carry (host reference of
+    k_gate_states)."""
+    c = carry
+    out = np.empty(len(pred), np.uint8)
+    for i, p in enumerate(pred):
+        k = k0 + i
+        fr = (1, NONE, k, NONE, NONE) if (p & 1) else (0, k, NONE, NONE, k if (p & 2) else NONE)
+        c = gs_apply(c, fr, D)
+        out[i] = 2 if c[1] > c[2] else 1
+    return out
+
+
+def carry_in(summaries_global: Sequence, rank: int, D: int):
+    """Carry at the first frame of ``rank``'s summary range, from the summaries
+    (global frame indices) of ranks 0..rank-1."""
+    c = C1_IDLE
+    for q in range(rank):
+        c = gs_apply(c, summaries_global[q], D)
+    return c
+
+
+# ---------------------------------------------------------------------------
+# shard geometry
+# ---------------------------------------------------------------------------
+
+@dataclass
+class Shard:
+    rank: int
+    world: int
+    b: int            # first local frame (global index): own frames minus warm-up
+    k0: int           # first emitted frame
+    k1: int           # one past the last emitted frame
+    tf_frames: int    # frames [b, b + tf_frames) form this rank's gate summary
+    lo: int           # input slice [lo, hi) (samples of the stream)
+    hi: int
+    p0: int           # output range [p0, p1) (samples of the stream)
+    p1: int
+    geometry: Dict = field(default_factory=dict)   # GatePipeline geometry (local)
+    chunk_lo: int = 0                              # global index of local chunk 0
+
+
+def plan_shards(N: int, n_fft: int, hop: int, world: int, seg: int = GATE_SEGMENT,
+                flush: int = 48000 * 5) -> List[Shard]:
+    """Cut the standard-mode frames of an N-sample stream into ``world`` shards."""
+    pad, pe, F, s0 = dsp.std_schedule(N, n_fft, hop)
+    W = -(-n_fft // hop) - 1                     # warm-up frames of the register OLA
+    bounds = dsp.std_flush_bounds(N, n_fft, hop, flush)
+    nch = max(1, len(bounds) - 1)
+    chunk_first = bounds[1] if len(bounds) > 2 else 0
+    chunk_len = (bounds[2] - bounds[1]) if len(bounds) > 3 else max(
+        1, (bounds[-1] - bounds[1]) if len(bounds) > 2 else 1)
+
+    def chunk_of(p):
+        if nch <= 1 or p < chunk_first:
+            return 0
+        return min(1 + (p - chunk_first) // chunk_len, nch - 1)
+
+    def sk(k):
+        return s0 + k * hop
+
+    # b_0 = 0, b_{r+1} = b_r + seg * m_r; rank r emits [k0_r, k0_{r+1}), k0_r = b_r + W
+    per = F / max(1, world)
+    bs = [0]
+    for r in range(1, world):
+        m = max(1, int(round((r * per - W) / seg)) - (bs[-1] // seg))
+        nb = bs[-1] + seg * m
+        if nb + W >= F - 1:
+            break
+        bs.append(nb)
+    R = len(bs)
+    k0s = [0] + [b + W for b in bs[1:]]
+    shards = []
+    for r in range(R):
+        b, k0 = bs[r], k0s[r]
+        last = r == R - 1
+        k1 = F if last else k0s[r + 1]
+        kl = k1 - 1                                  # last local frame
+        lo = max(0, sk(b))
+        hi = N if last else min(N, sk(kl) + n_fft)
+        p0 = 0 if r == 0 else sk(k0)
+        p1 = N if last else sk(k1)
+        c_lo, c_hi = chunk_of(p0), chunk_of(max(p0, p1 - 1))
+        n_loc = c_hi - c_lo + 1
+        geom = dict(first_start=sk(b) - lo, n_frames=kl - b + 1, out_begin=p0 - lo,
+                    out_len=p1 - p0, n_chunks=n_loc,
+                    chunk_first=(bounds[c_lo + 1] - lo) if n_loc > 1 else 0,
+                    chunk_len=chunk_len if n_loc > 1 else 1,
+                    bounds=[max(p0, bounds[c]) - lo for c in range(c_lo, c_hi + 1)] + [p1 - lo])
+        tf = (bs[r + 1] - b) if not last else (kl - b + 1)
+        shards.append(Shard(rank=r, world=R, b=b, k0=k0, k1=k1, tf_frames=tf, lo=lo, hi=hi,
+                            p0=p0, p1=p1, geometry=geom, chunk_lo=c_lo))
+    return shards
+
+
+def n_chunks_global(N: int, n_fft: int, hop: int, flush: int = 48000 * 5) -> int:
+    return max(1, len(dsp.std_flush_bounds(N, n_fft, hop, flush)) - 1)
+
+
+# ---------------------------------------------------------------------------
+# one rank's pipeline, phase by phase
+# ---------------------------------------------------------------------------
+
+class ShardRunner:
+    """The standard pipeline on one shard: levels -> gate summary | exchange |
+    gate from carry -> transform + chunk peaks | exchange | limiter fix-up."""
+
+    def __init__(self, x_slice, sr: int, shard: Shard, ch: int = 2, **params):
+        """``x_slice``: the shard's input samples [lo, hi), host [n, ch] array or
+        flat device float32 tensor (interleaved)."""
+        from . import engine
+        self.shard = shard
+        if hasattr(x_slice, "data_ptr"):
+            ss = engine.StreamSet(x=x_slice, offs=[0], lens=[x_slice.numel() // ch], ch=ch, sr=sr)
+        else:
+            ss = engine.StreamSet.from_arrays([x_slice], sr)
+        self.pipe = engine.GatePipeline(ss, geometry=[shard.geometry], **params)
+
+    # phase 1
+    def summary(self):
+        """Levels, then this rank's gate summary in global frame indices."""
+        import ctypes as C
+        from ._lib import check, lib, ptr, stream_handle, F32
+        L, P, hs = lib(), self.pipe.plan.h, stream_handle()
+        check(L.tomatis_levels(P, ptr(self.pipe.ss.x), ptr(self.pipe.r), F32, hs), "levels")
+        nseg = int(L.tomatis_plan_gate_segments(P))
+        buf = np.zeros((max(1, nseg), 5), np.int32)
+        check(L.tomatis_gate_segment_sums(P, ptr(self.pipe.r),
+                                          buf.ctypes.data_as(C.c_void_p), hs), "gate_segment_sums")
+        D = self.pipe.up_delay_frames
+        n_tf_segs = -(-self.shard.tf_frames // GATE_SEGMENT)
+        S = gs_identity()
+        for i in range(min(n_tf_segs, nseg)):
+            S = gs_cat(S, tuple(int(v) for v in buf[i]), D)
+        self.local_sums = buf[:nseg]
+        return gs_shift(S, self.shard.b)
+
+    # phase 2
+    def gate_and_transform(self, summaries_global):
+        """Gate from the composed carry, then the transform; returns the local
+        chunk peaks (uint32 float bits) placed in a global chunk array."""
+        import ctypes as C
+        from ._lib import check, lib, ptr, stream_handle
+        L, P, hs = lib(), self.pipe.plan.h, stream_handle()
+        D = self.pipe.up_delay_frames
+        c = carry_shift(carry_in(summaries_global, self.shard.rank, D), -self.shard.b)
+        carry = np.asarray(c, np.int32)
+        pp = self.pipe
+        check(L.tomatis_gate_std_carry(P, ptr(pp.r), carry.ctypes.data_as(C.c_void_p),
+                                       ptr(pp.states), ptr(pp.rows), hs), "gate_std_carry")
+        pp.peaks.zero_()
+        check(L.tomatis_stft_ola(P, ptr(pp.ss.x), ptr(pp.gains), pp.n_rows, ptr(pp.rows),
+                                 ptr(pp.y), ptr(pp.peaks), hs), "stft_ola")
+        return pp.peaks
+
+    # phase 3
+    def limit(self, peaks_local):
+        from ._lib import check, lib, ptr, stream_handle
+        from .engine import PEAK_LIMIT
+        L, P, hs = lib(), self.pipe.plan.h, stream_handle()
+        pp = self.pipe
+        pp.peaks.copy_(peaks_local)
+        check(L.tomatis_apply_limiter(P, ptr(pp.y), ptr(pp.peaks), PEAK_LIMIT, hs), "limiter")
+        return pp.result()
+
+
+def run_emulated(x: np.ndarray, sr: int, world: int, **params):
+    """All shards of one stream in this process, exchanges done on the host.
+    Returns (y [N, ch], states [F], per-chunk peaks as float) — the same values
+    a ``world``-rank run produces."""
+    import torch
+    N, ch = x.shape
+    n_fft, hop = params["n_fft"], params["hop"]
+    shards = plan_shards(N, n_fft, hop, world)
+    runners = [ShardRunner(x[s.lo:s.hi], sr, s, ch=ch, **params) for s in shards]
+    sums = [rn.summary() for rn in runners]
+    G = n_chunks_global(N, n_fft, hop)
+    gpk = np.zeros(G, np.uint32)
+    loc = []
+    for rn in runners:
+        pk = rn.gate_and_transform(sums).cpu().numpy().astype(np.uint32)
+        n = rn.shard.geometry["n_chunks"]
+        c0 = rn.shard.chunk_lo
+        gpk[c0:c0 + n] = np.maximum(gpk[c0:c0 + n], pk[:n])
+        loc.append((c0, n))
+    ys, sts = [], []
+    for rn, (c0, n) in zip(runners, loc):
+        res = rn.limit(torch.from_numpy(gpk[c0:c0 + n].astype(np.int32)).to(rn.pipe.peaks.device))
+        ys.append(res.output(0))
+        s = rn.shard
+        st = res.stream_states(0)
+        sts.append(st[s.k0 - s.b:s.k1 - s.b])
+    torch.cuda.synchronize()
+    return np.concatenate(ys), np.concatenate(sts), gpk.view(np.float32)
+
+
+# ---------------------------------------------------------------------------
+# distributed run: one shard per rank (torch.distributed; RCCL on device
+# tensors with the nccl backend, gloo on CPU tensors in the tests)
+# ---------------------------------------------------------------------------
+
+def exchange_summaries(S, device=None):
+    """all_gather of this rank's 5-int summary -> list of every rank's."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(S, dtype=torch.int64, device=device)
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return [tuple(int(v) for v in t.cpu())]
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [tuple(int(v) for v in o.cpu()) for o in out]
+
+
+def exchange_peaks(global_bits: np.ndarray, device=None) -> np.ndarray:
+    """all_reduce(MAX) of per-chunk peak bits (non-negative floats order as
+    their bit patterns)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.from_numpy(global_bits.astype(np.int64)).to(device or "cpu")
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.cpu().numpy().astype(np.uint32)
+
+
+def run_rank(x_slice, sr: int, N: int, rank: int, world: int, ch: int = 2, device="cuda",
+             **params):
+    """This rank's shard of an N-sample stream (``x_slice`` = samples
+    [shard.lo, shard.hi), host array or device tensor).  Returns (shard, Result).
+    Collectives: one all_gather (gate summaries), one all_reduce (chunk peaks)."""
+    import torch
+    n_fft, hop = params["n_fft"], params["hop"]
+    shards = plan_shards(N, n_fft, hop, world)
+    if len(shards) != world:
+        raise ValueError(f"stream too short for {world} shards")
+    sh = shards[rank]
+    rn = ShardRunner(x_slice, sr, sh, ch=ch, **params)
+    sums = exchange_summaries(rn.summary(), device=device)
+    pk = rn.gate_and_transform(sums).cpu().numpy().astype(np.uint32)
+    G = n_chunks_global(N, n_fft, hop)
+    g = np.zeros(G, np.uint32)
+    n = sh.geometry["n_chunks"]
+    g[sh.chunk_lo:sh.chunk_lo + n] = pk[:n]
+    g = exchange_peaks(g, device=device)
+    res = rn.limit(torch.from_numpy(g[sh.chunk_lo:sh.chunk_lo + n].astype(np.int32))
+                   .to(rn.pipe.peaks.device))
+    return sh, res
