@@ -40,6 +40,11 @@ WORKLOADS = {
            "C4: 64 x 5 min stereo 48 kHz per GPU (512 over 8 GPUs), standard, 2048/512"),
     "c5x": (16, 300, 96000, 2, "xfade", 4096, 1024,
             "C5 stage 1: 16 x 5 min stereo 96 kHz per GPU, xfade 500 ms, 4096/1024"),
+    # strong scaling: ONE 60-min stream time-sharded over all ranks
+    "c2ts": (1, 3600, 44100, 2, "timeshard", 2048, 512,
+             "C2 time-sharded: one 60 min stereo 44.1 kHz stream split over all ranks, "
+             "standard mode, n_fft 2048 hop 512 (gate-summary all_gather + chunk-peak "
+             "all_reduce)"),
 }
 
 
@@ -109,10 +114,20 @@ def main():
 
     nstr, secs, sr, ch, mode, n_fft, hop, desc = WORKLOADS[a.workload]
     n = secs * sr
-    ss = engine.StreamSet.synthetic(nstr, n, ch, sr, seed0=1000 + rank * nstr)
+    if mode == "timeshard":
+        from tomatis_audio_processor_amd import timeshard
+        from tomatis_audio_processor_amd._lib import check, lib, ptr, stream_handle
+        sh = timeshard.plan_shards(n, n_fft, hop, ws)[rank]
+        xs = torch.empty((sh.hi - sh.lo) * ch, dtype=torch.float32, device="cuda")
+        check(lib().tomatis_synth_fill(ptr(xs), sh.hi - sh.lo, ch, sr, 1000, sh.lo,
+                                       stream_handle()), "synth_fill")
+        pipe = timeshard.RankStep(xs, sr, n, rank, ws, ch=ch, gate_ui=50, n_fft=n_fft, hop=hop)
+        ss = pipe.rn.pipe.ss
+    else:
+        ss = engine.StreamSet.synthetic(nstr, n, ch, sr, seed0=1000 + rank * nstr)
     if mode == "standard":
         pipe = engine.GatePipeline(ss, gate_ui=50, n_fft=n_fft, hop=hop)
-    else:
+    elif mode == "xfade":
         pipe = engine.GatePipeline(ss, gate_ui=50, gate_offset=-90, n_fft=n_fft, hop=hop,
                                    xfade_ms=500.0)
     torch.cuda.synchronize()
@@ -155,30 +170,33 @@ def main():
         man = torch.cat(allm)
     man = man.cpu().numpy()
 
-    samples_per_step = n * ch * nstr * ws
+    strong = mode == "timeshard"
+    samples_per_step = n * ch * nstr * (1 if strong else ws)
     value = samples_per_step * a.steps / elapsed / 1e6
     ms_per_step = elapsed / a.steps * 1e3
     # roofline of the dominant kernel (fused STFT-OLA), per launch on this rank
-    alg_bytes = 8.0 * n * ch * nstr
+    alg_bytes = 8.0 * (ss.lens[0] * ch if strong else n * ch * nstr)
     achieved_gbs = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = load_traffic(a.workload)
-    flops = flops_per_ch_sample(n_fft, hop) * n * ch * nstr
+    flops = flops_per_ch_sample(n_fft, hop) * alg_bytes / 8.0
     tflops = flops / (kern_ms * 1e-3) / 1e12
 
     if rank == 0:
         cpu = None
-        if a.cpu_sample_s > 0 and mode == "standard":
+        if a.cpu_sample_s > 0 and mode == "standard" and not strong:
             xs = ss.x[:a.cpu_sample_s * sr * ch].cpu().numpy().reshape(-1, ch)
             cpu = cpu_baseline(a.cpu_sample_s, sr, n_fft, hop, ch, x_host=xs)
         out = {
             "metric": "Msamples/s (44.1 kHz stereo) end-to-end STFT-gate-OLA; % HBM roofline",
             "value": round(value, 1), "unit": "Msamples/s", "n_gpus": ws, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (seeded device-generated noise, -20/-60 dBFS alternating 1.5 s)",
             "config": {"workload": desc, "streams_per_gpu": nstr, "samples_per_channel": n,
                        "channels": ch, "sr": sr, "mode": mode, "n_fft": n_fft, "hop": hop,
-                       "parallelism": f"file-parallel x{ws} (RCCL manifest all_gather)"},
+                       "parallelism": (f"time-sharded x{ws} (RCCL gate all_gather + peak "
+                                       f"all_reduce)" if strong else
+                                       f"file-parallel x{ws} (RCCL manifest all_gather)")},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,

@@ -229,7 +229,7 @@ class ShardRunner:
         return gs_shift(S, self.shard.b)
 
     # phase 2
-    def gate_and_transform(self, summaries_global):
+    def gate_and_transform(self, summaries_global, marks=None):
         """Gate from the composed carry, then the transform; returns the local
         chunk peaks (uint32 float bits) placed in a global chunk array."""
         import ctypes as C
@@ -242,8 +242,12 @@ class ShardRunner:
         check(L.tomatis_gate_std_carry(P, ptr(pp.r), carry.ctypes.data_as(C.c_void_p),
                                        ptr(pp.states), ptr(pp.rows), hs), "gate_std_carry")
         pp.peaks.zero_()
+        if marks:
+            marks[0].record()
         check(L.tomatis_stft_ola(P, ptr(pp.ss.x), ptr(pp.gains), pp.n_rows, ptr(pp.rows),
                                  ptr(pp.y), ptr(pp.peaks), hs), "stft_ola")
+        if marks:
+            marks[1].record()
         return pp.peaks
 
     # phase 3
@@ -337,3 +341,34 @@ def run_rank(x_slice, sr: int, N: int, rank: int, world: int, ch: int = 2, devic
     res = rn.limit(torch.from_numpy(g[sh.chunk_lo:sh.chunk_lo + n].astype(np.int32))
                    .to(rn.pipe.peaks.device))
     return sh, res
+
+
+class RankStep:
+    """One rank's shard, set up once; ``run()`` = one pass with both exchanges
+    (bench.py workload c2ts)."""
+
+    def __init__(self, x_slice, sr: int, N: int, rank: int, world: int, ch: int = 2,
+                 device="cuda", **params):
+        import torch
+        shards = plan_shards(N, params["n_fft"], params["hop"], world)
+        if len(shards) != world:
+            raise ValueError(f"stream too short for {world} shards")
+        self.sh = shards[rank]
+        self.rn = ShardRunner(x_slice, sr, self.sh, ch=ch, **params)
+        self.G = n_chunks_global(N, params["n_fft"], params["hop"])
+        self.device = device
+        self.torch = torch
+
+    def run(self, marks=None):
+        sh, rn = self.sh, self.rn
+        sums = exchange_summaries(rn.summary(), device=self.device)
+        pk = rn.gate_and_transform(sums, marks).cpu().numpy().astype(np.uint32)
+        g = np.zeros(self.G, np.uint32)
+        n = sh.geometry["n_chunks"]
+        g[sh.chunk_lo:sh.chunk_lo + n] = pk[:n]
+        g = exchange_peaks(g, device=self.device)
+        return rn.limit(self.torch.from_numpy(g[sh.chunk_lo:sh.chunk_lo + n].astype(np.int32))
+                        .to(rn.pipe.peaks.device))
+
+    def result(self):
+        return self.rn.pipe.result()
