@@ -81,3 +81,39 @@ def test_small_runs_vs_oracle():
     m = ref["wsum"][ref["pad"]:ref["pad"] + N] >= 1e-3
     err = np.abs(outs[0][m] - ref["y"][m])
     assert float(err.max()) <= 1e-4
+
+
+@pytest.mark.parametrize("n_fft,hop,sr,xfade_ms", [(2048, 512, 48000, 500.0), (4096, 1024, 96000, 500.0),
+                                                   (2048, 512, 44100, 0.0), (4096, 2048, 48000, 30.0)])
+def test_xfade_alpha_parallel_matches_sequential(n_fft, hop, sr, xfade_ms):
+    """The three-pass segment-parallel alpha scan equals the sequential float64
+    recurrence bit for bit (alpha, gain rows, hence samples)."""
+    torch, E = _engine()
+    lens = [sr * 200 + 11, sr * 45 + 777]
+    xs = [synth_stream(900 + i, n, 2, sr) for i, n in enumerate(lens)]
+
+    def run(env):
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update({k: str(v) for k, v in env.items()})
+        try:
+            ss = E.StreamSet.from_arrays(xs, sr)
+            pipe = E.GatePipeline(ss, gate_ui=50, gate_offset=-90, n_fft=n_fft, hop=hop,
+                                  xfade_ms=xfade_ms)
+            res = pipe.run()
+            torch.cuda.synchronize()
+            return ([res.stream_alpha(i) for i in range(len(xs))],
+                    [res.output(i) for i in range(len(xs))],
+                    pipe.rows[:pipe.plan.total_frames].cpu().numpy())
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+
+    a_seq, y_seq, r_seq = run({"TOMATIS_ALPHA_SEQ": 1})
+    a_par, y_par, r_par = run({})
+    assert np.array_equal(r_par, r_seq)
+    for i in range(len(xs)):
+        assert a_par[i].tobytes() == a_seq[i].tobytes()
+        assert y_par[i].tobytes() == y_seq[i].tobytes()

@@ -502,6 +502,117 @@ __device__ __forceinline__ double alpha_step(double a, double tgt, double step) 
 }
 
 // xfade (process_tomatis_xfade.py:251-274): alpha starts at 0.0.
+// xfade alpha (process_tomatis_xfade.py:251-274) in three passes over the gate
+// segments.  alpha moves by +-step toward the frame's target (0 in C1, 1 in C2)
+// and snaps to it once within step, so after J = xf + 2 consecutive frames of
+// one state it equals that target exactly, whatever it was before (frames
+// before 0 count as C1: alpha starts at 0.0).  From a segment's first such
+// "sync" frame on, alpha depends only on the states; only the prefix before it
+// needs the previous segment's final alpha.  Every value is produced by the
+// same float64 operations in the same order as the sequential reference loop.
+__device__ __forceinline__ uint16_t xfade_row(double a, int xf) {
+  if (xf > 0 && a > 0.0 && a < 1.0) return (uint16_t)(2 + (int)rint(a * xf));
+  return (a < 0.5) ? 0 : 1;
+}
+
+// pass 1: one thread per segment: sync frame, alpha from it to the segment end
+__global__ __launch_bounds__(64) void k_alpha_sync(const TomatisStream* __restrict__ st,
+                                                   const GateSeg* __restrict__ segs, int nseg,
+                                                   const uint8_t* __restrict__ states, int xf,
+                                                   uint16_t* __restrict__ rows,
+                                                   double* __restrict__ alpha,
+                                                   int32_t* __restrict__ seg_q,
+                                                   double* __restrict__ seg_final) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nseg) return;
+  const GateSeg G = segs[i];
+  const TomatisStream S = st[G.s];
+  const uint8_t* stt = states + S.frame_base;
+  const int J = xf + 2;
+  const double step = xf > 0 ? 1.0 / xf : 1.0;
+  // run of equal states ending just before k0 (frames < 0 are C1 forever)
+  uint8_t prev = 1;
+  int run = J;
+  if (G.k0 > 0) {
+    prev = stt[G.k0 - 1];
+    run = 1;
+    int64_t k = G.k0 - 2;
+    for (; k >= 0 && run < J && stt[k] == prev; --k) ++run;
+    if (k < 0 && run < J && prev == 1) run = J;  // reaches the C1 pre-history
+  }
+  int q = G.nf;
+  for (int j = 0; j < G.nf; ++j) {
+    const uint8_t t = stt[G.k0 + j];
+    run = (t == prev) ? min(run + 1, J) : 1;
+    prev = t;
+    if (xf == 0 || run >= J) {
+      q = j;
+      break;
+    }
+  }
+  seg_q[i] = q;
+  if (q == G.nf) return;
+  double a = stt[G.k0 + q] == 1 ? 0.0 : 1.0;
+  for (int j = q; j < G.nf; ++j) {
+    const int64_t f = S.frame_base + G.k0 + j;
+    const double tgt = stt[G.k0 + j] == 1 ? 0.0 : 1.0;
+    if (j > q) a = (xf > 0) ? alpha_step(a, tgt, step) : tgt;
+    if (alpha) alpha[f] = a;
+    rows[f] = xfade_row(a, xf);
+  }
+  seg_final[i] = a;
+}
+
+// pass 2: one thread per stream: carry-in alpha of every segment
+__global__ void k_alpha_chain(const TomatisStream* __restrict__ st, int n_streams,
+                              const GateSeg* __restrict__ segs, const int32_t* __restrict__ seg_first,
+                              const int32_t* __restrict__ seg_count,
+                              const uint8_t* __restrict__ states, int xf,
+                              const int32_t* __restrict__ seg_q,
+                              const double* __restrict__ seg_final, double* __restrict__ carry_in) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_streams) return;
+  const TomatisStream S = st[s];
+  const double step = xf > 0 ? 1.0 / xf : 1.0;
+  double c = 0.0;
+  for (int i = seg_first[s], e = seg_first[s] + seg_count[s]; i < e; ++i) {
+    carry_in[i] = c;
+    const GateSeg G = segs[i];
+    if (seg_q[i] < G.nf) {
+      c = seg_final[i];
+    } else {  // no sync frame: the whole segment from the carry
+      for (int j = 0; j < G.nf; ++j) {
+        const double tgt = states[S.frame_base + G.k0 + j] == 1 ? 0.0 : 1.0;
+        c = (xf > 0) ? alpha_step(c, tgt, step) : tgt;
+      }
+    }
+  }
+}
+
+// pass 3: one thread per segment: the frames before its sync frame
+__global__ __launch_bounds__(64) void k_alpha_prefix(const TomatisStream* __restrict__ st,
+                                                     const GateSeg* __restrict__ segs, int nseg,
+                                                     const uint8_t* __restrict__ states, int xf,
+                                                     const int32_t* __restrict__ seg_q,
+                                                     const double* __restrict__ carry_in,
+                                                     uint16_t* __restrict__ rows,
+                                                     double* __restrict__ alpha) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nseg) return;
+  const GateSeg G = segs[i];
+  const TomatisStream S = st[G.s];
+  const double step = xf > 0 ? 1.0 / xf : 1.0;
+  double a = carry_in[i];
+  for (int j = 0; j < seg_q[i]; ++j) {
+    const int64_t f = S.frame_base + G.k0 + j;
+    const double tgt = states[f] == 1 ? 0.0 : 1.0;
+    a = (xf > 0) ? alpha_step(a, tgt, step) : tgt;
+    if (alpha) alpha[f] = a;
+    rows[f] = xfade_row(a, xf);
+  }
+}
+
+// sequential reference of the three passes (kept for TOMATIS_ALPHA_SEQ=1)
 __global__ void k_alpha_xfade(const TomatisStream* __restrict__ st, int n_streams,
                               const uint8_t* __restrict__ states, int xf,
                               uint16_t* __restrict__ rows, double* __restrict__ alpha) {
@@ -794,6 +905,9 @@ struct tomatis_plan_s {
   void* gsum = nullptr;
   void* gcarry = nullptr;
   void* gcarry_in = nullptr;  // time shards: carry-in per stream
+  int32_t* aq = nullptr;      // xfade alpha passes: sync frame per gate segment
+  double* afin = nullptr;     //   alpha at the segment end (when synced)
+  double* acin = nullptr;     //   carry-in alpha per segment
   // streaming levels (hop % 128 == 0): per-stream 8-block groups and leaves
   bool leaf_path = false;
   int64_t n_groups = 0;
@@ -855,6 +969,7 @@ int tomatis_plan_destroy(tomatis_plan_t p) {
                   p->seg_start, p->win, p->win2, p->winv, p->twN, p->twP, p->scratch,
                   p->pos_base, p->chunks, p->mh_tf, p->mh_cnt, p->mh_off, p->gperm,
                   p->grp_base, p->leaf_base, p->leaves, p->gsum, p->gcarry, p->gcarry_in,
+                  p->aq, p->afin, p->acin,
                   p->chunk_need, p->chunk_done, p->chunk_rng, p->err};
   for (void* q : ptrs) dfree(q);
   delete p;
@@ -1364,8 +1479,26 @@ int tomatis_gate_std(tomatis_plan_t p, const float* r, uint8_t* states, uint16_t
                        p->segs, p->n_segs, D, p->seg_start, states, xf ? nullptr : rows);
   }
   if (xf) {
-    hipLaunchKernelGGL(k_alpha_xfade, dim3((p->n_streams + 63) / 64), dim3(64), 0, s, p->st,
-                       p->n_streams, states, p->d.xfade_frames, rows, alpha_out);
+    const int nxf = p->d.xfade_frames;
+    if (env_int("TOMATIS_ALPHA_SEQ", 0) != 0) {
+      hipLaunchKernelGGL(k_alpha_xfade, dim3((p->n_streams + 63) / 64), dim3(64), 0, s, p->st,
+                         p->n_streams, states, nxf, rows, alpha_out);
+      return launch_check();
+    }
+    if (!p->aq) {
+      if (hipMalloc(reinterpret_cast<void**>(&p->aq), (size_t)p->n_segs * sizeof(int32_t)) ||
+          hipMalloc(reinterpret_cast<void**>(&p->afin), (size_t)p->n_segs * sizeof(double)) ||
+          hipMalloc(reinterpret_cast<void**>(&p->acin), (size_t)p->n_segs * sizeof(double)))
+        return TOMATIS_E_NOMEM;
+    }
+    const unsigned gs = (unsigned)((p->n_segs + 63) / 64);
+    hipLaunchKernelGGL(k_alpha_sync, dim3(gs), dim3(64), 0, s, p->st, p->segs, p->n_segs, states,
+                       nxf, rows, alpha_out, p->aq, p->afin);
+    hipLaunchKernelGGL(k_alpha_chain, dim3((p->n_streams + 63) / 64), dim3(64), 0, s, p->st,
+                       p->n_streams, p->segs, p->seg_first, p->seg_count, states, nxf, p->aq,
+                       p->afin, p->acin);
+    hipLaunchKernelGGL(k_alpha_prefix, dim3(gs), dim3(64), 0, s, p->st, p->segs, p->n_segs,
+                       states, nxf, p->aq, p->acin, rows, alpha_out);
   }
   return launch_check();
 }
