@@ -386,7 +386,7 @@ class AdaptivePipeline:
         self.n_rows = len(rows)
         self.out_offs = out_offs
 
-    def run(self):
+    def run(self, marks=None):
         torch = _torch()
         L, P, hs = lib(), self.plan.h, stream_handle()
         ss = self.ss
@@ -439,8 +439,12 @@ class AdaptivePipeline:
                                        ptr(self.rows), ptr(self.alpha), hs), "minhold_bisect")
         # 4. STFT-gain-OLA, normalise max(w,1e-8), restore, global limiter
         self.peaks.zero_()
+        if marks:
+            marks[0].record()
         check(L.tomatis_stft_ola(P, ptr(ss.x), ptr(self.gains), self.n_rows, ptr(self.rows),
                                  ptr(self.y), ptr(self.peaks), hs), "stft_ola")
+        if marks:
+            marks[1].record()
         check(L.tomatis_apply_limiter(P, ptr(self.y), ptr(self.peaks), PEAK_LIMIT, hs),
               "apply_limiter")
         self.prec = prec
@@ -501,11 +505,15 @@ class StaticEqPipeline:
         self.gains = torch.from_numpy(np.asarray(gain_bins, np.float32)[None, :].copy()).to(dev)
         self.out_offs = out_offs
 
-    def run(self):
+    def run(self, marks=None):
         L, P, hs = lib(), self.plan.h, stream_handle()
         self.peaks.zero_()
+        if marks:
+            marks[0].record()
         check(L.tomatis_stft_ola(P, ptr(self.ss.x), ptr(self.gains), 1, ptr(self.rows),
                                  ptr(self.y), ptr(self.peaks), hs), "stft_ola")
+        if marks:
+            marks[1].record()
         return self.result()
 
     def result(self) -> Result:
