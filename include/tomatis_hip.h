@@ -30,6 +30,14 @@
  *   src/process_tomatis_adaptive.py:340-345
  *   np.max(np.abs(x)) (adaptive :201,          tomatis_absmax
  *       layer2 gain protect :178,213)
+ *   src/compare_audio.py:12-24 (stft_mag_avg)    tomatis_an_spectra(MAG),
+ *                                                 tomatis_an_frame_mean
+ *   src/layer2_analyze_eq.py:54-88               tomatis_an_frame_r, tomatis_an_select,
+ *       (stft_logpower_median)                    tomatis_an_spectra(LOGPOW),
+ *                                                 tomatis_an_frame_median
+ *   src/validate_layer1.py:261-389               tomatis_an_frame_r, tomatis_an_select,
+ *       (compute_conditional_spectrum)            tomatis_an_spectra(RATIO),
+ *                                                 tomatis_an_frame_median
  *
  * Conventions: every call is asynchronous on the given hipStream_t and returns
  * an int status (0 = ok, <0 = error, see TOMATIS_E_*); no exceptions cross the
@@ -47,7 +55,7 @@
 extern "C" {
 #endif
 
-#define TOMATIS_ABI_VERSION 3
+#define TOMATIS_ABI_VERSION 4
 
 #define TOMATIS_OK 0
 #define TOMATIS_E_ARG (-1)        /* bad argument */
@@ -212,6 +220,53 @@ int tomatis_scale_copy(const float* x, float* y, int64_t n, float scale, void* h
  * samples [start, start+n) of stream `seed`, ch channels, interleaved. */
 int tomatis_synth_fill(float* x, int64_t n, int32_t ch, int32_t sr, uint32_t seed,
                        int64_t start, void* hip_stream);
+
+/* ---------------------------------------------------------------------------
+ * Analysis spectra (tm_analysis.hip).  Frames
+ * f = 0 .. F-1 start at sample f*hop, F = 1 + (n - n_fft) / hop (n >= n_fft);
+ * n_fft a power of two in [256, 8192]; x (and y) float32 [n][ch] interleaved.
+ * ------------------------------------------------------------------------- */
+#define TOMATIS_AN_LEVEL_CHMEAN 0     /* mono = sqrt(mean_c x_c^2)        validate_layer1.py:304-306 */
+#define TOMATIS_AN_LEVEL_POWER_MONO 1 /* mono = sqrt(0.5(L^2+R^2)+1e-12)  layer2_analyze_eq.py:71, compare_audio.py:7-10 */
+#define TOMATIS_AN_SIG_RAW 0          /* spectrum of x itself (ch must be 1)                    */
+#define TOMATIS_AN_SIG_POWER_MONO 1   /* spectrum of power_mono(x) (ch must be 2)               */
+#define TOMATIS_AN_MAG 0              /* |rfft(win*s)|                    compare_audio.py:16-21 */
+#define TOMATIS_AN_LOGPOW 1           /* 10 log10(|rfft(win*s)|^2+1e-12)  layer2_analyze_eq.py:76-79 */
+#define TOMATIS_AN_RATIO 2            /* mean_c|Y_c| / max(mean_c|X_c|, 1e-10)  validate_layer1.py:340-355 */
+
+/* Per-frame r = sqrt(mean(mono^2) + 1e-12) in numpy's pairwise order
+ * (bit-exact); x scaled by `scale` first.  r_out: F floats. */
+int tomatis_an_frame_r(const float* x, int64_t n, int32_t ch, int32_t n_fft, int32_t hop,
+                       int32_t level_mode, float scale, float* r_out, void* hip_stream);
+
+/* mask[f] = level predicate on r bits (dsp.gate_bits form) && (cls == NULL ||
+ * cls[f] == cls_want); keep_above = 1: level >= T <=> (b >= thr) xor b in exc;
+ * keep_above = 0: level > T <=> !((b <= thr) xor b in exc).  exc_host: up to 4
+ * host words.  count (device int32): number of kept frames. */
+int tomatis_an_select(const float* r, int32_t n_frames, uint32_t thr_bits,
+                      const uint32_t* exc_host, int32_t n_exc, int32_t keep_above,
+                      const int8_t* cls, int32_t cls_want, uint8_t* mask, int32_t* count,
+                      void* hip_stream);
+
+/* Per-frame spectra rows out[F][n_fft/2+1] (TOMATIS_AN_MAG / _LOGPOW of the
+ * signal chosen by sig_mode, scaled by `scale`; TOMATIS_AN_RATIO of y over x). */
+int tomatis_an_spectra(const float* x, const float* y, int64_t n, int32_t ch, int32_t n_fft,
+                       int32_t hop, int32_t kind, int32_t sig_mode, float scale,
+                       const float* win, float* out, void* hip_stream);
+
+/* out[k] = (sum over f in order of spec[f][k]) / F, float32 (np.mean(axis=0)). */
+int tomatis_an_frame_mean(const float* spec, int32_t n_frames, int32_t n_bins, float* out,
+                          void* hip_stream);
+
+/* Workspace (uint32 words) for tomatis_an_frame_median. */
+int64_t tomatis_an_median_work_words(int32_t n_bins);
+
+/* out[k] = np.median over the n_sel frames with mask[f] != 0 (mask NULL: all
+ * frames, n_sel = F) of spec[f][k]; even counts average the two middle values
+ * in float32 like numpy. */
+int tomatis_an_frame_median(const float* spec, int32_t n_frames, int32_t n_bins,
+                            const uint8_t* mask, int32_t n_sel, uint32_t* work, float* out,
+                            void* hip_stream);
 
 #ifdef __cplusplus
 }

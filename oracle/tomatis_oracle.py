@@ -583,3 +583,119 @@ def ceil_div(a, b):
 
 __all__ = [n for n in dir() if not n.startswith("_")] + ["_std_schedule"]
 _unused = math  # keep import for downstream users of math-based helpers
+
+
+# ----------------------------------------------------------------------------
+# Analysis spectra.  Same numpy primitives in the
+# same order as the reference loops; batched along frames where numpy is
+# order-identical (rfft / mean along the last axis, elementwise ops).
+# ----------------------------------------------------------------------------
+
+def power_mono(x_lr):
+    """compare_audio.py:7-10 (identical copy used by layer2_analyze_eq.py)."""
+    p = 0.5 * (x_lr[:, 0] ** 2 + x_lr[:, 1] ** 2)
+    return np.sqrt(p + EPS)
+
+
+def _full_frames(x, n_fft, hop, F):
+    """[F, n_fft(, ch)] view of frames starting at f*hop (all inside x)."""
+    if x.ndim == 1:
+        s0 = x.strides[0]
+        return as_strided(x, shape=(F, n_fft), strides=(hop * s0, s0), writeable=False)
+    s0, s1 = x.strides
+    return as_strided(x, shape=(F, n_fft, x.shape[1]), strides=(hop * s0, s0, s1),
+                      writeable=False)
+
+
+def stft_mag_avg(x, sr, n_fft=4096, hop=2048):
+    """compare_audio.stft_mag_avg (src/compare_audio.py:12-24)."""
+    win = np.hanning(n_fft).astype(np.float32)
+    F = 1 + (len(x) - n_fft) // hop
+    if F <= 0:
+        raise ValueError("need at least one array to stack")
+    fr = _full_frames(x, n_fft, hop, F) * win
+    mags = np.abs(np.fft.rfft(fr, axis=-1)).astype(np.float32)
+    return mags.mean(axis=0)
+
+
+def analyze_frame_r(x_lr, n_fft, hop):
+    """r of rms_dbfs(power_mono(frame)) per frame (layer2_analyze_eq.py:13-15,71-73)."""
+    F = 1 + (len(x_lr) - n_fft) // hop
+    mono = np.ascontiguousarray(_full_frames(power_mono(x_lr), n_fft, hop, F))
+    return np.sqrt(np.mean(mono * mono, axis=1) + EPS)
+
+
+def stft_logpower_median(x_lr, sr, n_fft, hop, music_dbfs):
+    """layer2_analyze_eq.stft_logpower_median (src/layer2_analyze_eq.py:54-88)."""
+    win = np.hanning(n_fft).astype(np.float32)
+    freqs = np.fft.rfftfreq(n_fft, 1.0 / sr)
+    F = 1 + (len(x_lr) - n_fft) // hop
+    if F <= 10:
+        raise ValueError("片段太短，无法做稳定频谱统计。")
+    r = analyze_frame_r(x_lr, n_fft, hop)
+    lv = (20.0 * np.log10(r + EPS)).astype(np.float64)
+    keep = ~(lv <= music_dbfs)
+    used = int(keep.sum())
+    if used < 50:
+        raise ValueError(f"可用音乐帧太少（{used} 帧）。把 --music_dbfs 调低一点（例如 -70）。")
+    mono = _full_frames(power_mono(x_lr), n_fft, hop, F)[keep]
+    X = np.fft.rfft(mono * win, axis=-1)
+    P = (X.real * X.real + X.imag * X.imag).astype(np.float32)
+    logs = (10.0 * np.log10(P + EPS)).astype(np.float32)
+    med = np.median(logs, axis=0).astype(np.float32)
+    return freqs, med, used
+
+
+def find_stable_frames(states, margin=2):
+    """validate_layer1.find_stable_frames (src/validate_layer1.py:245-258)."""
+    n = len(states)
+    c1, c2 = [], []
+    for i in range(margin, n - margin):
+        w = states[i - margin:i + margin + 1]
+        if all(s == "C1" for s in w):
+            c1.append(i)
+        elif all(s == "C2" for s in w):
+            c2.append(i)
+    return c1, c2
+
+
+def conditional_frame_r(x, n_fft, hop):
+    """r of rms_dbfs(sqrt(mean(frame**2, axis=1))) per frame f (start f*hop)."""
+    x = x.reshape(len(x), -1)
+    F = 1 + (len(x) - n_fft) // hop
+    return frame_r(_full_frames(np.ascontiguousarray(x), n_fft, hop, F))
+
+
+def compute_conditional_spectrum(x, y, sr, states, n_fft, hop, level_threshold=-60):
+    """validate_layer1.compute_conditional_spectrum (src/validate_layer1.py:261-389),
+    the second (effective) pair of loops at :338-375 and the median at :377-387."""
+    x = x.reshape(-1, 1) if x.ndim == 1 else x
+    y = y.reshape(-1, 1) if y.ndim == 1 else y
+    ch = x.shape[1]
+    c1s, c2s = find_stable_frames(states, margin=2)
+    freqs = np.fft.rfftfreq(n_fft, 1 / sr)
+    nb = len(freqs)
+    win = np.hanning(n_fft).astype(np.float32)
+    F = max(0, 1 + (len(x) - n_fft) // hop)
+    r = conditional_frame_r(x, n_fft, hop) if F > 0 else np.zeros(0, np.float32)
+    lv = (20.0 * np.log10(r + EPS)).astype(np.float64)
+    res = []
+    for lst in (c1s, c2s):
+        idx = np.asarray([i for i in lst if i * hop >= 0 and i * hop + n_fft <= len(x)],
+                         np.int64)
+        idx = idx[~(lv[idx] < level_threshold)] if len(idx) else idx
+        if len(idx) == 0:
+            res.append((np.zeros(nb), 0))
+            continue
+        X = np.zeros((len(idx), nb), dtype=np.float32)
+        Y = np.zeros((len(idx), nb), dtype=np.float32)
+        st = (idx * hop)[:, None] + np.arange(n_fft)[None, :]
+        for c in range(ch):
+            X += np.abs(np.fft.rfft(x[st, c] * win, axis=-1))
+            Y += np.abs(np.fft.rfft(y[st, c] * win, axis=-1))
+        X /= ch
+        Y /= ch
+        X = np.maximum(X, 1e-10)
+        med = np.median(Y / X, axis=0)
+        res.append((20 * np.log10(med + EPS), len(idx)))
+    return freqs, res[0][0], res[1][0], res[0][1], res[1][1]

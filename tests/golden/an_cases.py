@@ -1,0 +1,39 @@
+"""Analysis-spectrum golden cases, shared by
+tools/make_analysis_goldens.py (runs the reference) and the tests.
+
+Inputs are regenerated from seeds: ``an_inputs(case)`` returns the stereo/mono
+PCM (``synth_stream``), the validator's processed signal ``y`` (a fixed float32
+two-tap filter of x) and its state list (seeded C1/C2 runs)."""
+import numpy as np
+
+AN_CASES = [
+    dict(name="an_mag_48k_4096_2048", fn="stft_mag_avg", sr=48000, ch=2, N=48000 * 5 + 777,
+         seed=31, n_fft=4096, hop=2048),
+    dict(name="an_mag_44k_2048_512", fn="stft_mag_avg", sr=44100, ch=2, N=44100 * 3 + 259,
+         seed=32, n_fft=2048, hop=512),
+    dict(name="an_logpow_48k_8192_4096", fn="stft_logpower_median", sr=48000, ch=2,
+         N=48000 * 6 + 100, seed=33, n_fft=8192, hop=4096, music_dbfs=-65.0),
+    dict(name="an_logpow_48k_4096_1024_sel", fn="stft_logpower_median", sr=48000, ch=2,
+         N=48000 * 6, seed=34, n_fft=4096, hop=1024, music_dbfs=-40.0),
+    dict(name="an_logpow_48k_2048_512_even", fn="stft_logpower_median", sr=48000, ch=2,
+         N=48000 * 3, seed=37, n_fft=2048, hop=512, music_dbfs=-70.0),
+    dict(name="an_cond_44k_st_2048_512", fn="compute_conditional_spectrum", sr=44100, ch=2,
+         N=44100 * 6 + 333, seed=35, n_fft=2048, hop=512, level_threshold=-60.0),
+    dict(name="an_cond_48k_mono_4096_1024", fn="compute_conditional_spectrum", sr=48000, ch=1,
+         N=48000 * 6 + 9, seed=36, n_fft=4096, hop=1024, level_threshold=-50.0),
+]
+AN_BY_NAME = {c["name"]: c for c in AN_CASES}
+
+
+def an_inputs(c):
+    from tomatis_audio_processor_amd.synth import synth_stream
+    x = synth_stream(c["seed"], c["N"], c["ch"], c["sr"])
+    y = (np.float32(0.6) * x).astype(np.float32)
+    y[3:] += (np.float32(0.25) * x[:-3]).astype(np.float32)
+    rng = np.random.default_rng(c["seed"])
+    n_states = 1 + c["N"] // c["hop"]
+    states, cur = [], "C1"
+    while len(states) < n_states:
+        states += [cur] * int(rng.integers(2, 30))
+        cur = "C2" if cur == "C1" else "C1"
+    return x, y, states[:n_states]

@@ -14,7 +14,7 @@ import ctypes as C
 import os
 
 LIB_NAME = "libtomatis_hip.so"
-ABI_VERSION = 3  # include/tomatis_hip.h TOMATIS_ABI_VERSION
+ABI_VERSION = 4  # include/tomatis_hip.h TOMATIS_ABI_VERSION
 GATE_SEGMENT = 1024      # TOMATIS_GATE_SEGMENT
 GATE_NONE = -536870912   # TOMATIS_GATE_NONE
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -78,6 +78,16 @@ _SIGS = {
     "tomatis_scale_copy": (C.c_int, [_P, _P, C.c_int64, C.c_float, _P]),
     "tomatis_synth_fill": (C.c_int, [_P, C.c_int64, C.c_int32, C.c_int32, C.c_uint32,
                                      C.c_int64, _P]),
+    # analysis spectra
+    "tomatis_an_frame_r": (C.c_int, [_P, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                     C.c_float, _P, _P]),
+    "tomatis_an_select": (C.c_int, [_P, C.c_int32, C.c_uint32, C.POINTER(C.c_uint32), C.c_int32,
+                                    C.c_int32, _P, C.c_int32, _P, _P, _P]),
+    "tomatis_an_spectra": (C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
+                                     C.c_int32, C.c_int32, C.c_float, _P, _P, _P]),
+    "tomatis_an_frame_mean": (C.c_int, [_P, C.c_int32, C.c_int32, _P, _P]),
+    "tomatis_an_median_work_words": (C.c_int64, [C.c_int32]),
+    "tomatis_an_frame_median": (C.c_int, [_P, C.c_int32, C.c_int32, _P, C.c_int32, _P, _P, _P]),
 }
 EXPORTS = tuple(_SIGS)
 

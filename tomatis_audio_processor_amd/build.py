@@ -1,13 +1,15 @@
 """Build ``libtomatis_hip.so`` in-tree with hipcc for gfx950 (no cmake/ninja needed).
 
-Two translation units, compiled in parallel and linked into one C-ABI library:
+Three translation units, compiled in parallel and linked into one C-ABI library:
 
 * ``tm_kernels.hip``   levels, gate, limiter, plan and the ``extern "C"`` entry points;
 * ``tm_transform.hip`` the fused transform kernels, compiled with the max-ILP
   machine scheduler (``-amdgpu-sched-strategy=max-ilp``), which keeps the
   per-frame LDS table reads batched instead of serialising them.  The other unit
   keeps the default scheduler so the streaming kernels stay at low register
-  counts (high occupancy).
+  counts (high occupancy);
+* ``tm_analysis.hip``  analysis spectra for the validators / calibration tools
+  (SURVEY.md §8 rows f3/f4).
 """
 from __future__ import annotations
 
@@ -23,6 +25,7 @@ SCHED = os.environ.get("TOMATIS_TRANSFORM_SCHED", "")
 UNITS = {  # source -> extra flags
     "tm_kernels.hip": [],
     "tm_transform.hip": ["-mllvm", f"-amdgpu-sched-strategy={SCHED}"] if SCHED else [],
+    "tm_analysis.hip": [],
 }
 DEPS = [os.path.join(CSRC, f) for f in (*UNITS, "tm_common.h", "tm_fft.h", "tm_shared.h")] + \
        [os.path.join(ROOT, "include", "tomatis_hip.h")]
