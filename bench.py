@@ -137,7 +137,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
-    ap.add_argument("--cpu-sample-s", type=int, default=900,
+    ap.add_argument("--cpu-sample-s", type=int, default=3600,
                     help="seconds of audio for the CPU baseline (0 disables)")
     a = ap.parse_args()
 
