@@ -27,6 +27,12 @@ def _gpu():
         pytest.skip("no GPU")
 
 
+def _written(out):
+    """The processors write FLAC (native codec); the reference's WAV fallback
+    name is used only if FLAC encoding failed."""
+    return out if os.path.exists(out) else out.replace(".flac", ".wav")
+
+
 def _wav(tmp_path, name, x, sr):
     p = str(tmp_path / name)
     audio_io.write(p, x, sr, "WAV", "FLOAT")
@@ -49,7 +55,7 @@ def test_process_tomatis_cli(tmp_path):
     rc = process_tomatis.main(["-i", inp, "-o", out, "--n_fft", "2048", "--hop", "512",
                                "--state_csv", st_csv])
     assert rc == 0
-    y, sr2 = audio_io.read(out.replace(".flac", ".wav"))
+    y, sr2 = audio_io.read(_written(out))
     ref = orc.process_standard(x, sr, gate_ui=50, n_fft=2048, hop=512)
     m = (ref["wsum"][ref["pad"]:ref["pad"] + N] >= 1e-3)
     _cmp(y, ref["y"], m)
@@ -116,13 +122,13 @@ def test_layer2_cli_gain_protect(tmp_path):
     layer2_apply_eq.main(["-i", inp, "-o", out, "--eq_csv", eq, "--n_fft", "2048", "--hop", "512"])
     fr, db = parse_eq_csv(eq_csv_rows())
     ref = orc.apply_eq_stft(x, sr, fr, db, n_fft=2048, hop=512)
-    y, _ = audio_io.read(out.replace(".flac", ".wav"))
+    y, _ = audio_io.read(_written(out))
     assert y.shape == ref["y"].shape
     # PCM_24 clips the reference's ill-conditioned head samples (F7): compare the rest
     m = (ref["wsum"] >= 1e-3)[:, None] & (np.abs(ref["y"]) < 0.99)
     _cmp(y, ref["y"], m)
     if ref["y_gp"] is not None:
-        assert os.path.exists(out.replace(".flac", "_gp.wav"))
+        assert os.path.exists(_written(out.replace(".flac", "_gp.flac")))
 
 
 def test_batch_runner_single_process(tmp_path):
@@ -145,3 +151,22 @@ def test_batch_runner_single_process(tmp_path):
         N = len(x)
         _cmp(y, ref["y"], ref["wsum"][ref["pad"]:ref["pad"] + N] >= 1e-3)
         assert man["streams"][i]["c2_frames"] == int(np.count_nonzero(ref["states"] == 2))
+
+
+def test_process_tomatis_flac_in_flac_out(tmp_path):
+    """FLAC PCM_24 in -> FLAC PCM_24 out through the native codec (row f1)."""
+    _gpu()
+    from tomatis_audio_processor_amd import process_tomatis
+    sr, N = 48000, 48000 * 4 + 77
+    x = synth_stream(105, N, 2, sr)
+    inp = str(tmp_path / "in.flac")
+    audio_io.write(inp, x, sr, "FLAC", "PCM_24")
+    xq, _ = audio_io.read(inp)  # what the processor sees (PCM_24 values)
+    out = str(tmp_path / "out.flac")
+    assert process_tomatis.main(["-i", inp, "-o", out, "--n_fft", "2048", "--hop", "512"]) == 0
+    assert os.path.exists(out) and not os.path.exists(out.replace(".flac", ".wav"))
+    y, sr2 = audio_io.read(out)
+    assert sr2 == sr and y.shape == (N, 2)
+    ref = orc.process_standard(xq, sr, gate_ui=50, n_fft=2048, hop=512)
+    m = ref["wsum"][ref["pad"]:ref["pad"] + N] >= 1e-3
+    _cmp(y, ref["y"], m)

@@ -72,9 +72,13 @@ def test_wav_roundtrip(tmp_path):
     assert np.array_equal(z, x)
 
 
-def test_flac_fallback_to_wav(tmp_path):
+def test_flac_fallback_to_wav(tmp_path, monkeypatch):
     if audio_io.have_soundfile():
         pytest.skip("libsndfile present: FLAC is written directly")
+
+    def fail(*a, **k):
+        raise audio_io.AudioFormatError("encoder unavailable")
+    monkeypatch.setattr(audio_io, "_write_flac", fail)  # reference branch :242-251
     x = synth_stream(4, 1000, 2, 48000)
     out = str(tmp_path / "o.flac")
     path, is_flac = audio_io.write_with_fallback(out, x, 48000, log=lambda m: None)

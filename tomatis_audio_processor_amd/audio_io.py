@@ -1,18 +1,21 @@
 """Audio file I/O for the drop-in CLIs (codec boundary).
 
 ``soundfile`` (libsndfile) is used when importable, exactly like the
-reference (FLAC PCM_24 output).  The build image has no libsndfile, so a
-built-in RIFF/WAVE codec covers PCM 8/16/24/32 and IEEE float 32/64 input and
-PCM_24 / float output.  Writing FLAC without libsndfile raises, which sends the
-processors down the reference's own fallback branch: write
-``out_path.replace(".flac", ".wav")`` as WAV PCM_24
-(src/process_tomatis.py:242-251).
+reference (FLAC PCM_24 output).  The build image has no libsndfile, so the
+package carries its own codecs: FLAC through the native host library
+``libtomatis_flac.so`` (``csrc/tm_flac.cpp``, C ABI ``include/tomatis_flac.h``:
+lossless encode of PCM 8..32, decode of any FLAC stream with CRC checks) and a
+built-in RIFF/WAVE codec (PCM 8/16/24/32 and IEEE float 32/64 input, PCM_24 /
+PCM_16 / float output).  If FLAC encoding fails, the processors take the
+reference's own fallback branch: write ``out_path.replace(".flac", ".wav")`` as
+WAV PCM_24 (src/process_tomatis.py:242-251).
 
 Sample conversion follows libsndfile's normalisation: int -> float divides by
 2^(bits-1); float -> PCM_24 multiplies by 0x7FFFFF and rounds to nearest.
 """
 from __future__ import annotations
 
+import ctypes as C
 import os
 import struct
 
@@ -36,18 +39,128 @@ def have_soundfile() -> bool:
     return _sf is not None
 
 
+# ---------------------------------------------------------------------------
+# native FLAC (libtomatis_flac.so)
+# ---------------------------------------------------------------------------
+_FLAC = None
+FLAC_LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libtomatis_flac.so")
+
+
+def _flac():
+    global _FLAC
+    if _FLAC is None:
+        if not os.path.exists(FLAC_LIB):
+            raise AudioFormatError(f"{FLAC_LIB} not built (tomatis_audio_processor_amd.build"
+                                   ".build_flac)")
+        h = C.CDLL(FLAC_LIB)
+        P, I32, I64 = C.c_void_p, C.c_int32, C.c_int64
+        h.tomatis_flac_encode.argtypes = [P, I64, I32, I32, I32, C.POINTER(C.POINTER(C.c_uint8)),
+                                          C.POINTER(I64)]
+        h.tomatis_flac_free.argtypes = [C.POINTER(C.c_uint8)]
+        h.tomatis_flac_free.restype = None
+        h.tomatis_flac_info.argtypes = [P, I64, C.POINTER(I32), C.POINTER(I32), C.POINTER(I32),
+                                        C.POINTER(I64)]
+        h.tomatis_flac_decode.argtypes = [P, I64, P, I64, C.POINTER(I64)]
+        _FLAC = h
+    return _FLAC
+
+
+_FLAC_ERR = {-1: "bad argument", -2: "not a FLAC stream / unsupported", -3: "CRC mismatch",
+             -4: "out of memory"}
+
+
+def flac_encode_int(pcm: np.ndarray, sr: int, bps: int) -> bytes:
+    """Lossless FLAC stream of int32 PCM [frames, ch] at ``bps`` bits."""
+    pcm = np.ascontiguousarray(pcm, np.int32)
+    if pcm.ndim == 1:
+        pcm = pcm[:, None]
+    out = C.POINTER(C.c_uint8)()
+    n = C.c_int64()
+    rc = _flac().tomatis_flac_encode(pcm.ctypes.data, pcm.shape[0], pcm.shape[1], sr, bps,
+                                     C.byref(out), C.byref(n))
+    if rc:
+        raise AudioFormatError(f"FLAC encode failed: {_FLAC_ERR.get(rc, rc)}")
+    try:
+        return C.string_at(out, n.value)
+    finally:
+        _flac().tomatis_flac_free(out)
+
+
+def flac_info_bytes(data: bytes):
+    sr, ch, bps, n = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int64()
+    rc = _flac().tomatis_flac_info(data, len(data), C.byref(sr), C.byref(ch), C.byref(bps),
+                                   C.byref(n))
+    if rc:
+        raise AudioFormatError(f"FLAC: {_FLAC_ERR.get(rc, rc)}")
+    return sr.value, ch.value, bps.value, n.value
+
+
+def flac_decode_int(data: bytes):
+    """(int32 PCM [frames, ch], sr, bps) of an in-memory FLAC stream."""
+    sr, ch, bps, n = flac_info_bytes(data)
+    pcm = np.empty((n, ch), np.int32)
+    got = C.c_int64()
+    rc = _flac().tomatis_flac_decode(data, len(data), pcm.ctypes.data, n, C.byref(got))
+    if rc:
+        raise AudioFormatError(f"FLAC decode failed: {_FLAC_ERR.get(rc, rc)}")
+    return pcm[:got.value], sr, bps
+
+
+def _read_flac(path: str):
+    with open(path, "rb") as f:
+        data = f.read()
+    pcm, sr, bps = flac_decode_int(data)
+    # libsndfile's int -> float normalisation: v / 2^(bps-1)
+    x = (pcm.astype(np.float64) / float(1 << (bps - 1))).astype(np.float32)
+    return np.ascontiguousarray(x), sr
+
+
+def _write_flac(path: str, data: np.ndarray, sr: int, subtype: str = "PCM_24"):
+    st = subtype.upper()
+    if st == "PCM_24":
+        v = np.clip(np.rint(np.asarray(data, np.float64) * 8388607.0), -8388608, 8388607)
+        bps = 24
+    elif st == "PCM_16":
+        v = np.clip(np.rint(np.asarray(data, np.float64) * 32767.0), -32768, 32767)
+        bps = 16
+    else:
+        raise AudioFormatError(f"FLAC subtype {subtype} not supported")
+    blob = flac_encode_int(v.astype(np.int32), sr, bps)
+    with open(path, "wb") as f:
+        f.write(blob)
+
+
+def _sniff(path: str):
+    """Container by content, like libsndfile (the reference writes FLAC to
+    whatever name ``-o`` gives, src/process_tomatis_xfade.py:115)."""
+    try:
+        with open(path, "rb") as f:
+            m = f.read(4)
+    except OSError:
+        return None
+    return {b"fLaC": "flac", b"RIFF": "wav", b"RF64": "wav"}.get(m)
+
+
 def info(path: str):
     """(samplerate, channels, frames) without decoding the samples."""
     if _sf is not None and not path.lower().endswith(".wav"):
         i = _sf.info(path)
         return i.samplerate, i.channels, i.frames
+    if _sniff(path) == "flac":
+        with open(path, "rb") as f:
+            head = f.read(42)
+        sr, ch, _, n = flac_info_bytes(head)
+        return sr, ch, n
     fmt, ch, sr, bits, data_off, data_len = _parse_wav_header(path)
     return sr, ch, data_len // (ch * (bits // 8))
 
 
 def read(path: str):
     """Decode a file to float32 [frames, channels] and its sample rate."""
-    if path.lower().endswith(".wav"):
+    kind = _sniff(path)
+    if kind == "flac" and _sf is None:
+        return _read_flac(path)
+    if kind == "wav" or path.lower().endswith(".wav"):
         return _read_wav(path)
     if _sf is None:
         raise AudioFormatError(f"cannot decode {os.path.basename(path)}: libsndfile (soundfile) "
@@ -65,7 +178,10 @@ def write(path: str, data: np.ndarray, sr: int, fmt: str = "FLAC", subtype: str 
         _write_wav(path, data, sr, subtype)
         return
     if _sf is None:
-        raise AudioFormatError("FLAC encoding needs libsndfile (soundfile), not installed")
+        if fmt.upper() != "FLAC":
+            raise AudioFormatError(f"format {fmt} needs libsndfile (soundfile), not installed")
+        _write_flac(path, data, sr, subtype)
+        return
     _sf.write(path, data, sr, format=fmt, subtype=subtype)
 
 

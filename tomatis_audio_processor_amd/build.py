@@ -72,9 +72,29 @@ def build(force: bool = False, verbose: bool = True, out: str = OUT, extra=()) -
     return out
 
 
+FLAC_SRC = os.path.join(CSRC, "tm_flac.cpp")
+FLAC_OUT = os.path.join(HERE, "libtomatis_flac.so")
+
+
+def build_flac(force: bool = False, verbose: bool = True) -> str:
+    """Host FLAC codec: plain C++, built with g++."""
+    deps = [FLAC_SRC, os.path.join(ROOT, "include", "tomatis_flac.h"), os.path.abspath(__file__)]
+    if (not force and os.path.exists(FLAC_OUT)
+            and all(os.path.getmtime(d) <= os.path.getmtime(FLAC_OUT) for d in deps)):
+        return FLAC_OUT
+    cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-Wall", "-shared", "-fPIC",
+           "-o", FLAC_OUT + ".tmp", FLAC_SRC]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(FLAC_OUT + ".tmp", FLAC_OUT)
+    return FLAC_OUT
+
+
 if __name__ == "__main__":
     # python -m tomatis_audio_processor_amd.build [--force] [--out PATH -- extra hipcc flags]
     a = sys.argv[1:]
     extra = a[a.index("--") + 1:] if "--" in a else []
     out = a[a.index("--out") + 1] if "--out" in a else OUT
     build(force="--force" in a, out=out, extra=extra)
+    build_flac(force="--force" in a)
