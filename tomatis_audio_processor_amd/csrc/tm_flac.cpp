@@ -10,8 +10,8 @@
 // arithmetic that touches sample values.
 //
 // Encoder: fixed 4096-sample blocks, per channel the cheapest of CONSTANT,
-// FIXED order 0..4 (Rice / Rice2 partitioned residual, partition order and
-// parameters by exact bit count) and VERBATIM; stereo also tries the
+// FIXED (order by the smallest |residual| sum; Rice / Rice2 partitioned
+// residual, partition order and parameters from partition sums) and VERBATIM; stereo also tries the
 // left/side, side/right and mid/side decorrelations.  STREAMINFO carries
 // min/max block and frame sizes and total samples; MD5 is left zero
 // ("unknown", allowed by the format).  Decoder: the full frame/subframe
@@ -23,6 +23,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <functional>
+#include <thread>
 #include <vector>
 
 #include "../../include/tomatis_flac.h"
@@ -170,50 +172,58 @@ struct RicePlan {
   uint64_t bits = ~0ull;
 };
 
-// exact residual bits for the best partition order / parameters
+// Rice partition order / parameters from per-partition sums of the zigzag
+// residual (libFLAC-style estimate: bits(k) ~ cnt*(k+1) + (sum >> k)); sums of
+// the finest partitions are computed once and merged for coarser orders.
 RicePlan plan_rice(const int64_t* r, int n, int order) {
   RicePlan best;
-  std::vector<uint64_t> u(n);
-  for (int i = order; i < n; ++i) u[i] = zz(r[i]);
-  for (int po = 0; po <= kMaxPart; ++po) {
-    if (n % (1 << po)) break;
-    const int ps = n >> po;
-    if (ps <= order) break;
+  int pmax = 0;
+  while (pmax < kMaxPart && n % (1 << (pmax + 1)) == 0 && (n >> (pmax + 1)) > order) ++pmax;
+  const int np = 1 << pmax, ps = n >> pmax;
+  uint64_t sum[1 << kMaxPart], mx[1 << kMaxPart];
+  int cnt[1 << kMaxPart];
+  for (int p = 0; p < np; ++p) {
+    const int a = p == 0 ? order : p * ps, b = (p + 1) * ps;
+    uint64_t sm = 0, m = 0;
+    for (int i = a; i < b; ++i) {
+      const uint64_t u = zz(r[i]);
+      sm += u;
+      m = std::max(m, u);
+    }
+    sum[p] = sm;
+    mx[p] = m;
+    cnt[p] = b - a;
+  }
+  for (int po = pmax; po >= 0; --po) {
+    const int parts = 1 << po;
     RicePlan pl;
     pl.porder = po;
     uint64_t tot = 2 + 4;
     bool need5 = false;
-    for (int p = 0; p < (1 << po); ++p) {
-      const int a = p == 0 ? order : p * ps, b = (p + 1) * ps;
-      const int cnt = b - a;
-      uint64_t sum = 0;
-      for (int i = a; i < b; ++i) sum += u[i];
-      int k0 = 0;
-      if (cnt > 0) {
-        const uint64_t mean = sum / (uint64_t)cnt;
-        while (k0 < 30 && (1ull << (k0 + 1)) <= mean) ++k0;
+    for (int p = 0; p < parts; ++p) {
+      const uint64_t sm = sum[p], m = mx[p];
+      const int c = cnt[p];
+      int k = 0;
+      if (c > 0) {
+        const uint64_t mean = sm / (uint64_t)c;
+        while (k < 30 && (1ull << (k + 1)) <= mean) ++k;
       }
-      uint64_t bb = ~0ull;
-      int bk = 0;
-      for (int k = std::max(0, k0 - 1); k <= std::min(30, k0 + 1); ++k) {
-        uint64_t c = (uint64_t)cnt * (k + 1);
-        for (int i = a; i < b; ++i) c += u[i] >> k;
-        if (c < bb) {
-          bb = c;
-          bk = k;
-        }
-      }
-      uint64_t umax = 0;
-      for (int i = a; i < b; ++i) umax = std::max(umax, u[i]);
-      if ((umax >> bk) >= (1ull << 24)) bb = 1ull << 60;  // absurd quotient: never chosen
-      pl.k[p] = bk;
-      need5 |= bk > 14;
+      uint64_t bb = (uint64_t)c * (k + 1) + (sm >> k);
+      if ((m >> k) >= (1ull << 24)) bb = 1ull << 60;  // absurd quotient: never chosen
+      pl.k[p] = k;
+      need5 |= k > 14;
       tot += bb;
     }
     pl.method = need5 ? 1 : 0;
-    tot += (uint64_t)(1 << po) * (need5 ? 5 : 4);
+    tot += (uint64_t)parts * (need5 ? 5 : 4);
     pl.bits = tot;
     if (tot < best.bits) best = pl;
+    // merge pairs for the next coarser order
+    for (int p = 0; p < parts / 2; ++p) {
+      sum[p] = sum[2 * p] + sum[2 * p + 1];
+      mx[p] = std::max(mx[2 * p], mx[2 * p + 1]);
+      cnt[p] = cnt[2 * p] + cnt[2 * p + 1];
+    }
   }
   return best;
 }
@@ -254,16 +264,36 @@ SubPlan plan_subframe(const int64_t* s, int n, int bps, std::vector<int64_t>& re
   best.kind = 1;
   best.bits = 8 + (uint64_t)n * bps;
   res.resize(n);
-  for (int order = 0; order <= 4 && order < n; ++order) {
-    fixed_residual(s, n, order, res.data());
-    RicePlan rp = plan_rice(res.data(), n, order);
-    const uint64_t bits = 8 + (uint64_t)order * bps + rp.bits;
-    if (bits < best.bits) {
-      best.kind = 2;
-      best.order = order;
-      best.rice = rp;
-      best.bits = bits;
+  // fixed order by the smallest sum |residual| (one pass per order), then the
+  // Rice plan of that order only
+  // (all five orders in one pass over successive differences, from sample 4)
+  int bo = 0;
+  if (n > 4) {
+    uint64_t e[5] = {0, 0, 0, 0, 0};
+    int64_t d1p = s[3] - s[2], d2p = d1p - (s[2] - s[1]);
+    int64_t d3p = d2p - ((s[2] - s[1]) - (s[1] - s[0]));
+    for (int i = 4; i < n; ++i) {
+      const int64_t d0 = s[i], d1 = s[i] - s[i - 1], d2 = d1 - d1p, d3 = d2 - d2p, d4 = d3 - d3p;
+      e[0] += (uint64_t)(d0 < 0 ? -d0 : d0);
+      e[1] += (uint64_t)(d1 < 0 ? -d1 : d1);
+      e[2] += (uint64_t)(d2 < 0 ? -d2 : d2);
+      e[3] += (uint64_t)(d3 < 0 ? -d3 : d3);
+      e[4] += (uint64_t)(d4 < 0 ? -d4 : d4);
+      d1p = d1;
+      d2p = d2;
+      d3p = d3;
     }
+    for (int o = 1; o < 5; ++o)
+      if (e[o] < e[bo]) bo = o;
+  }
+  fixed_residual(s, n, bo, res.data());
+  RicePlan rp = plan_rice(res.data(), n, bo);
+  const uint64_t bits = 8 + (uint64_t)bo * bps + rp.bits;
+  if (bits < best.bits) {
+    best.kind = 2;
+    best.order = bo;
+    best.rice = rp;
+    best.bits = bits;
   }
   return best;
 }
@@ -308,33 +338,34 @@ int ss_code(int bps) {
   }
 }
 
-}  // namespace
-
-extern "C" {
-
-int tomatis_flac_encode(const int32_t* pcm, int64_t frames, int32_t ch, int32_t sr, int32_t bps,
-                        uint8_t** out, int64_t* out_len) {
-  if (!out || !out_len || (frames > 0 && !pcm) || frames < 0 || ch < 1 || ch > 8 || sr < 1 ||
-      sr > 655350 || bps < 4 || bps > 32 || frames >= (1ll << 36))
-    return TOMATIS_FLAC_E_ARG;
-  const int64_t lim = bps == 32 ? INT32_MAX : (1ll << (bps - 1)) - 1;
-  BitWriter w;
-  w.put(0x664C6143u, 32);  // "fLaC"
-  const size_t si_pos = w.bytes();
-  w.put(1u << 7, 8);  // last metadata block, STREAMINFO
-  w.put(34, 24);
-  for (int i = 0; i < 34; ++i) w.put(0, 8);  // patched below
-  std::vector<int64_t> s[8], side, mid, res;
+// Encode blocks [b0, b1) (frame numbers = block indices) into w; frames are
+// byte-aligned, so per-thread outputs concatenate into the stream.
+struct EncStats {
   uint32_t min_fs = ~0u, max_fs = 0;
   int min_bs = kBlock, max_bs = 0;
+  int rc = TOMATIS_FLAC_OK;
+};
+
+void encode_blocks(const int32_t* pcm, int64_t frames, int ch, int bps, int64_t b0, int64_t b1,
+                   BitWriter& w, EncStats& st) {
+  const int64_t lim = bps == 32 ? INT32_MAX : (1ll << (bps - 1)) - 1;
+  std::vector<int64_t> s[8], side, mid, res;
+  uint32_t& min_fs = st.min_fs;
+  uint32_t& max_fs = st.max_fs;
+  int& min_bs = st.min_bs;
+  int& max_bs = st.max_bs;
   const Crc& C = crc();
-  for (int64_t f0 = 0, fn = 0; f0 < frames; f0 += kBlock, ++fn) {
+  for (int64_t fn = b0; fn < b1; ++fn) {
+    const int64_t f0 = fn * kBlock;
     const int n = (int)std::min<int64_t>(kBlock, frames - f0);
     for (int c = 0; c < ch; ++c) {
       s[c].resize(n);
       for (int i = 0; i < n; ++i) {
         const int64_t v = pcm[(f0 + i) * ch + c];
-        if (v > lim || v < -lim - 1) return TOMATIS_FLAC_E_ARG;
+        if (v > lim || v < -lim - 1) {
+          st.rc = TOMATIS_FLAC_E_ARG;
+          return;
+        }
         s[c][i] = v;
       }
     }
@@ -414,7 +445,47 @@ int tomatis_flac_encode(const int32_t* pcm, int64_t frames, int32_t ch, int32_t 
     max_fs = std::max(max_fs, fs);
     min_bs = std::min(min_bs, n);
     max_bs = std::max(max_bs, n);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int tomatis_flac_encode(const int32_t* pcm, int64_t frames, int32_t ch, int32_t sr, int32_t bps,
+                        uint8_t** out, int64_t* out_len) {
+  if (!out || !out_len || (frames > 0 && !pcm) || frames < 0 || ch < 1 || ch > 8 || sr < 1 ||
+      sr > 655350 || bps < 4 || bps > 32 || frames >= (1ll << 36))
+    return TOMATIS_FLAC_E_ARG;
+  // blocks are independent: contiguous block ranges on host threads
+  const int64_t nblk = (frames + kBlock - 1) / kBlock;
+  int nt = (int)std::min<int64_t>(std::max(1u, std::thread::hardware_concurrency()), 16);
+  if (const char* e = getenv("TOMATIS_FLAC_THREADS")) nt = std::max(1, atoi(e));
+  nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, nblk / 8));
+  std::vector<BitWriter> ws(nt);
+  std::vector<EncStats> sts(nt);
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t) {
+    const int64_t b0 = nblk * t / nt, b1 = nblk * (t + 1) / nt;
+    if (t == nt - 1)
+      encode_blocks(pcm, frames, ch, bps, b0, b1, ws[t], sts[t]);
+    else
+      th.emplace_back(encode_blocks, pcm, frames, ch, bps, b0, b1, std::ref(ws[t]),
+                      std::ref(sts[t]));
   }
+  for (auto& x : th) x.join();
+  EncStats tot;
+  size_t body = 0;
+  for (int t = 0; t < nt; ++t) {
+    if (sts[t].rc) return sts[t].rc;
+    tot.min_fs = std::min(tot.min_fs, sts[t].min_fs);
+    tot.max_fs = std::max(tot.max_fs, sts[t].max_fs);
+    tot.min_bs = std::min(tot.min_bs, sts[t].min_bs);
+    tot.max_bs = std::max(tot.max_bs, sts[t].max_bs);
+    body += ws[t].bytes();
+  }
+  uint32_t min_fs = tot.min_fs, max_fs = tot.max_fs;
+  int min_bs = tot.min_bs, max_bs = tot.max_bs;
   if (frames == 0) min_fs = max_fs = 0, min_bs = max_bs = kBlock;
   // STREAMINFO (the min block size of a stream whose last block is short is
   // the nominal block size, as the format requires for fixed-blocksize streams)
@@ -429,12 +500,22 @@ int tomatis_flac_encode(const int32_t* pcm, int64_t frames, int32_t ch, int32_t 
   si.put((uint64_t)frames >> 32, 4);
   si.put((uint64_t)frames & 0xFFFFFFFFu, 32);
   for (int i = 0; i < 16; ++i) si.put(0, 8);
-  memcpy(w.buf.data() + si_pos + 4, si.buf.data(), 34);
-  uint8_t* o = (uint8_t*)malloc(w.bytes());
+  const size_t hdr = 4 + 4 + 34;
+  uint8_t* o = (uint8_t*)malloc(hdr + body);
   if (!o) return TOMATIS_FLAC_E_NOMEM;
-  memcpy(o, w.buf.data(), w.bytes());
+  memcpy(o, "fLaC", 4);
+  o[4] = 0x80;  // last metadata block, STREAMINFO, length 34
+  o[5] = 0;
+  o[6] = 0;
+  o[7] = 34;
+  memcpy(o + 8, si.buf.data(), 34);
+  size_t pos = hdr;
+  for (int t = 0; t < nt; ++t) {
+    memcpy(o + pos, ws[t].buf.data(), ws[t].bytes());
+    pos += ws[t].bytes();
+  }
   *out = o;
-  *out_len = (int64_t)w.bytes();
+  *out_len = (int64_t)(hdr + body);
   return TOMATIS_FLAC_OK;
 }
 
