@@ -233,3 +233,19 @@ def test_decoder_vs_independent_writer(assign):
     pcm, sr, b = audio_io.flac_decode_int(blob)
     assert (sr, b) == (48000, bps)
     assert np.array_equal(pcm, np.concatenate(frames).astype(np.int32))
+
+
+def test_threaded_decode_and_encode_exact(monkeypatch):
+    """Block ranges (encoder) and byte ranges with sync search (decoder) on
+    several host threads give the same stream / samples as one thread."""
+    rng = np.random.default_rng(11)
+    n = 48000 * 40
+    x = (rng.standard_normal((n, 2)) * 2e5).astype(np.int32)
+    monkeypatch.setenv("TOMATIS_FLAC_THREADS", "1")
+    b1 = audio_io.flac_encode_int(x, 48000, 24)
+    y1, _, _ = audio_io.flac_decode_int(b1)
+    monkeypatch.setenv("TOMATIS_FLAC_THREADS", "5")
+    b5 = audio_io.flac_encode_int(x, 48000, 24)
+    assert b5 == b1 and len(b1) > 5 * (1 << 20)
+    y5, _, _ = audio_io.flac_decode_int(b5)
+    assert np.array_equal(y1, x) and np.array_equal(y5, x)

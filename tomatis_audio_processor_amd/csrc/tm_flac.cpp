@@ -448,6 +448,194 @@ void encode_blocks(const int32_t* pcm, int64_t frames, int ch, int bps, int64_t 
     }
 }
 
+// One frame at d[p]: decoded into pcm at its own sample offset (frame number x
+// nominal block size for fixed-blocksize streams, the coded sample number
+// otherwise).  *consumed = frame bytes, *end = offset + block size.
+int decode_frame(const uint8_t* d, size_t len, size_t p, int ch0, int bps0, int64_t nominal,
+                 int32_t* pcm, int64_t max_frames, std::vector<int64_t>* sub, size_t* consumed,
+                 int64_t* end) {
+  const Crc& C = crc();
+  BitReader r(d + p, len - p);
+  if (r.get(14) != 0x3FFE) return TOMATIS_FLAC_E_FORMAT;
+  if (r.get(1)) return TOMATIS_FLAC_E_FORMAT;
+  const int strategy = (int)r.get(1);
+  const int bsc = (int)r.get(4), src = (int)r.get(4), asg = (int)r.get(4), ssc = (int)r.get(3);
+  if (r.get(1)) return TOMATIS_FLAC_E_FORMAT;
+  // UTF-8 coded frame / sample number
+  uint64_t num = r.get(8);
+  if (num & 0x80) {
+    int extra = 0;
+    while (extra < 7 && (num & (0x40 >> extra))) ++extra;
+    if (extra == 0) return TOMATIS_FLAC_E_FORMAT;
+    num &= (0x3Fu >> extra);
+    for (int i = 0; i < extra; ++i) {
+      const uint64_t c = r.get(8);
+      if ((c & 0xC0) != 0x80) return TOMATIS_FLAC_E_FORMAT;
+      num = (num << 6) | (c & 0x3F);
+    }
+  }
+  int n;
+  if (bsc == 1) n = 192;
+  else if (bsc >= 2 && bsc <= 5) n = 576 << (bsc - 2);
+  else if (bsc == 6) n = (int)r.get(8) + 1;
+  else if (bsc == 7) n = (int)r.get(16) + 1;
+  else if (bsc >= 8) n = 256 << (bsc - 8);
+  else return TOMATIS_FLAC_E_FORMAT;
+  if (src == 12) r.get(8);
+  else if (src == 13 || src == 14) r.get(16);
+  else if (src == 15) return TOMATIS_FLAC_E_FORMAT;
+  static const int ss_tab[8] = {0, 8, 12, 0, 16, 20, 24, 32};
+  const int bps = ssc == 0 ? bps0 : ss_tab[ssc];
+  if (bps == 0) return TOMATIS_FLAC_E_FORMAT;
+  const size_t hbytes = r.pos / 8;
+  const uint8_t hcrc = (uint8_t)r.get(8);
+  if (r.bad || C.crc8(d + p, hbytes) != hcrc) return TOMATIS_FLAC_E_CRC;
+    const int nch = asg < 8 ? asg + 1 : 2;
+    if (asg > 10 || nch != ch0) return TOMATIS_FLAC_E_FORMAT;
+    for (int c = 0; c < nch; ++c) {
+      std::vector<int64_t>& s = sub[c];
+      s.assign(n, 0);
+      int sb = bps;
+      if ((asg == 8 && c == 1) || (asg == 9 && c == 0) || (asg == 10 && c == 1)) ++sb;
+      if (r.get(1) != 0) return TOMATIS_FLAC_E_FORMAT;
+      const int type = (int)r.get(6);
+      int wasted = 0;
+      if (r.get(1)) wasted = (int)r.unary() + 1;
+      sb -= wasted;
+      if (sb <= 0) return TOMATIS_FLAC_E_FORMAT;
+      int order = 0;
+      if (type == 0) {
+        const int64_t c0 = r.get_signed(sb);
+        std::fill(s.begin(), s.end(), c0);
+      } else if (type == 1) {
+        for (int i = 0; i < n; ++i) s[i] = r.get_signed(sb);
+      } else if ((type & 0x38) == 0x08 || (type & 0x20)) {
+        const bool lpc = (type & 0x20) != 0;
+        order = lpc ? (type & 0x1F) + 1 : (type & 7);
+        if ((!lpc && order > 4) || order > n) return TOMATIS_FLAC_E_FORMAT;
+        for (int i = 0; i < order; ++i) s[i] = r.get_signed(sb);
+        int64_t coef[32] = {0};
+        int shift = 0;
+        if (lpc) {
+          const int prec = (int)r.get(4) + 1;
+          if (prec == 16) return TOMATIS_FLAC_E_FORMAT;
+          shift = (int)r.get_signed(5);
+          if (shift < 0) return TOMATIS_FLAC_E_FORMAT;
+          for (int i = 0; i < order; ++i) coef[i] = r.get_signed(prec);
+        }
+        // residual
+        const int method = (int)r.get(2);
+        if (method > 1) return TOMATIS_FLAC_E_FORMAT;
+        const int po = (int)r.get(4);
+        const int ps = n >> po;
+        if ((ps << po) != n || ps < order) return TOMATIS_FLAC_E_FORMAT;
+        const int pbits = method ? 5 : 4, esc = method ? 31 : 15;
+        int i = order;
+        for (int part = 0; part < (1 << po); ++part) {
+          const int k = (int)r.get(pbits);
+          const int end = (part + 1) * ps;
+          if (k == esc) {
+            const int nb = (int)r.get(5);
+            for (; i < end; ++i) s[i] = r.get_signed(nb);
+          } else {
+            for (; i < end; ++i) {
+              const uint64_t q = r.unary();
+              const uint64_t u = (q << k) | r.get(k);
+              s[i] = (int64_t)(u >> 1) ^ -(int64_t)(u & 1);
+            }
+          }
+          if (r.bad) return TOMATIS_FLAC_E_FORMAT;
+        }
+        // prediction
+        if (lpc) {
+          for (int t = order; t < n; ++t) {
+            int64_t acc = 0;
+            for (int j = 0; j < order; ++j) acc += coef[j] * s[t - 1 - j];
+            s[t] += acc >> shift;
+          }
+        } else {
+          for (int t = order; t < n; ++t) {
+            int64_t pr;
+            switch (order) {
+              case 0: pr = 0; break;
+              case 1: pr = s[t - 1]; break;
+              case 2: pr = 2 * s[t - 1] - s[t - 2]; break;
+              case 3: pr = 3 * s[t - 1] - 3 * s[t - 2] + s[t - 3]; break;
+              default: pr = 4 * s[t - 1] - 6 * s[t - 2] + 4 * s[t - 3] - s[t - 4]; break;
+            }
+            s[t] += pr;
+          }
+        }
+      } else {
+        return TOMATIS_FLAC_E_FORMAT;
+      }
+      if (wasted)
+        for (auto& x : s) x = (int64_t)((uint64_t)x << wasted);
+      if (r.bad) return TOMATIS_FLAC_E_FORMAT;
+    }
+    r.align();
+  const size_t fbytes = r.pos / 8;
+  const uint16_t fcrc = (uint16_t)r.get(16);
+  if (r.bad || C.crc16(d + p, fbytes) != fcrc) return TOMATIS_FLAC_E_CRC;
+  const int64_t off = strategy ? (int64_t)num : (int64_t)num * nominal;
+  // decorrelate and store
+  const int64_t take = std::min<int64_t>(n, std::max<int64_t>(0, max_frames - off));
+  for (int64_t i = 0; i < take; ++i) {
+    int64_t a = sub[0][i], b = nch > 1 ? sub[1][i] : 0;
+    if (asg == 8) b = a - b;                 // left, side -> right
+    else if (asg == 9) a = a + b;            // side, right -> left
+    else if (asg == 10) {                    // mid, side
+      const int64_t m = (a << 1) | (b & 1);
+      a = (m + b) >> 1;
+      b = (m - b) >> 1;
+    }
+    int32_t* o = pcm + (off + i) * nch;
+    o[0] = (int32_t)a;
+    if (nch > 1) o[1] = (int32_t)b;
+    for (int c = 2; c < nch; ++c) o[c] = (int32_t)sub[c][i];
+  }
+  *consumed = fbytes + 2;
+  *end = off + n;
+  return TOMATIS_FLAC_OK;
+}
+
+// Frames whose first byte lies in [lo, hi): the first one is found by sync
+// search (0xFFF8/0xFFF9 with a valid header and frame CRC), the rest follow.
+void decode_range(const uint8_t* d, size_t len, size_t lo, size_t hi, bool exact_start, int ch0,
+                  int bps0, int64_t nominal, int32_t* pcm, int64_t max_frames, int* rc,
+                  int64_t* end) {
+  std::vector<int64_t> sub[8];
+  size_t p = lo;
+  *rc = TOMATIS_FLAC_OK;
+  *end = 0;
+  if (!exact_start) {
+    while (true) {
+      while (p + 1 < hi && !(d[p] == 0xFF && (d[p + 1] & 0xFE) == 0xF8)) ++p;
+      if (p + 1 >= hi) return;  // no frame starts in this range
+      size_t used;
+      int64_t e;
+      if (decode_frame(d, len, p, ch0, bps0, nominal, pcm, max_frames, sub, &used, &e) ==
+          TOMATIS_FLAC_OK) {
+        *end = std::max(*end, e);
+        p += used;
+        break;
+      }
+      ++p;
+    }
+  }
+  while (p < hi && p + 2 <= len) {
+    size_t used;
+    int64_t e;
+    const int r = decode_frame(d, len, p, ch0, bps0, nominal, pcm, max_frames, sub, &used, &e);
+    if (r) {
+      *rc = r;
+      return;
+    }
+    *end = std::max(*end, e);
+    p += used;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -546,6 +734,7 @@ int tomatis_flac_decode(const uint8_t* d, int64_t len, int32_t* pcm, int64_t max
   int rc = tomatis_flac_info(d, len, &sr0, &ch0, &bps0, &total);
   if (rc) return rc;
   if (!pcm && max_frames > 0) return TOMATIS_FLAC_E_ARG;
+  const int64_t nominal = ((int64_t)d[10] << 8) | d[11];  // STREAMINFO max block size
   // skip metadata blocks
   size_t p = 4;
   while (true) {
@@ -555,147 +744,31 @@ int tomatis_flac_decode(const uint8_t* d, int64_t len, int32_t* pcm, int64_t max
     p += 4 + bl;
     if (last) break;
   }
-  const Crc& C = crc();
-  int64_t done = 0;
-  std::vector<int64_t> sub[8];
-  while (p + 2 <= (size_t)len && done < (total ? total : INT64_MAX)) {
-    BitReader r(d + p, (size_t)len - p);
-    if (r.get(14) != 0x3FFE) return TOMATIS_FLAC_E_FORMAT;
-    r.get(1);
-    r.get(1);  // blocking strategy (the decoder does not need it)
-    const int bsc = (int)r.get(4), src = (int)r.get(4), asg = (int)r.get(4),
-              ssc = (int)r.get(3);
-    r.get(1);
-    // UTF-8 coded frame / sample number
-    uint64_t v = r.get(8);
-    int extra = 0;
-    if (v & 0x80) {
-      while (extra < 7 && (v & (0x40 >> extra))) ++extra;
-      if (extra == 0) return TOMATIS_FLAC_E_FORMAT;
-      for (int i = 0; i < extra; ++i) r.get(8);
-    }
-    int n;
-    if (bsc == 1) n = 192;
-    else if (bsc >= 2 && bsc <= 5) n = 576 << (bsc - 2);
-    else if (bsc == 6) n = (int)r.get(8) + 1;
-    else if (bsc == 7) n = (int)r.get(16) + 1;
-    else if (bsc >= 8) n = 256 << (bsc - 8);
-    else return TOMATIS_FLAC_E_FORMAT;
-    if (src == 12) r.get(8);
-    else if (src == 13 || src == 14) r.get(16);
-    else if (src == 15) return TOMATIS_FLAC_E_FORMAT;
-    static const int ss_tab[8] = {0, 8, 12, 0, 16, 20, 24, 32};
-    const int bps = ssc == 0 ? bps0 : ss_tab[ssc];
-    if (bps == 0) return TOMATIS_FLAC_E_FORMAT;
-    const size_t hbytes = r.pos / 8;
-    const uint8_t hcrc = (uint8_t)r.get(8);
-    if (r.bad || C.crc8(d + p, hbytes) != hcrc) return TOMATIS_FLAC_E_CRC;
-    const int nch = asg < 8 ? asg + 1 : 2;
-    if (asg > 10 || nch != ch0) return TOMATIS_FLAC_E_FORMAT;
-    for (int c = 0; c < nch; ++c) {
-      std::vector<int64_t>& s = sub[c];
-      s.assign(n, 0);
-      int sb = bps;
-      if ((asg == 8 && c == 1) || (asg == 9 && c == 0) || (asg == 10 && c == 1)) ++sb;
-      if (r.get(1) != 0) return TOMATIS_FLAC_E_FORMAT;
-      const int type = (int)r.get(6);
-      int wasted = 0;
-      if (r.get(1)) wasted = (int)r.unary() + 1;
-      sb -= wasted;
-      if (sb <= 0) return TOMATIS_FLAC_E_FORMAT;
-      int order = 0;
-      if (type == 0) {
-        const int64_t c0 = r.get_signed(sb);
-        std::fill(s.begin(), s.end(), c0);
-      } else if (type == 1) {
-        for (int i = 0; i < n; ++i) s[i] = r.get_signed(sb);
-      } else if ((type & 0x38) == 0x08 || (type & 0x20)) {
-        const bool lpc = (type & 0x20) != 0;
-        order = lpc ? (type & 0x1F) + 1 : (type & 7);
-        if ((!lpc && order > 4) || order > n) return TOMATIS_FLAC_E_FORMAT;
-        for (int i = 0; i < order; ++i) s[i] = r.get_signed(sb);
-        int64_t coef[32] = {0};
-        int shift = 0;
-        if (lpc) {
-          const int prec = (int)r.get(4) + 1;
-          if (prec == 16) return TOMATIS_FLAC_E_FORMAT;
-          shift = (int)r.get_signed(5);
-          if (shift < 0) return TOMATIS_FLAC_E_FORMAT;
-          for (int i = 0; i < order; ++i) coef[i] = r.get_signed(prec);
-        }
-        // residual
-        const int method = (int)r.get(2);
-        if (method > 1) return TOMATIS_FLAC_E_FORMAT;
-        const int po = (int)r.get(4);
-        const int ps = n >> po;
-        if ((ps << po) != n || ps < order) return TOMATIS_FLAC_E_FORMAT;
-        const int pbits = method ? 5 : 4, esc = method ? 31 : 15;
-        int i = order;
-        for (int part = 0; part < (1 << po); ++part) {
-          const int k = (int)r.get(pbits);
-          const int end = (part + 1) * ps;
-          if (k == esc) {
-            const int nb = (int)r.get(5);
-            for (; i < end; ++i) s[i] = r.get_signed(nb);
-          } else {
-            for (; i < end; ++i) {
-              const uint64_t q = r.unary();
-              const uint64_t u = (q << k) | r.get(k);
-              s[i] = (int64_t)(u >> 1) ^ -(int64_t)(u & 1);
-            }
-          }
-          if (r.bad) return TOMATIS_FLAC_E_FORMAT;
-        }
-        // prediction
-        if (lpc) {
-          for (int t = order; t < n; ++t) {
-            int64_t acc = 0;
-            for (int j = 0; j < order; ++j) acc += coef[j] * s[t - 1 - j];
-            s[t] += acc >> shift;
-          }
-        } else {
-          for (int t = order; t < n; ++t) {
-            int64_t pr;
-            switch (order) {
-              case 0: pr = 0; break;
-              case 1: pr = s[t - 1]; break;
-              case 2: pr = 2 * s[t - 1] - s[t - 2]; break;
-              case 3: pr = 3 * s[t - 1] - 3 * s[t - 2] + s[t - 3]; break;
-              default: pr = 4 * s[t - 1] - 6 * s[t - 2] + 4 * s[t - 3] - s[t - 4]; break;
-            }
-            s[t] += pr;
-          }
-        }
-      } else {
-        return TOMATIS_FLAC_E_FORMAT;
-      }
-      if (wasted)
-        for (auto& x : s) x = (int64_t)((uint64_t)x << wasted);
-      if (r.bad) return TOMATIS_FLAC_E_FORMAT;
-    }
-    r.align();
-    const size_t fbytes = r.pos / 8;
-    const uint16_t fcrc = (uint16_t)r.get(16);
-    if (r.bad || C.crc16(d + p, fbytes) != fcrc) return TOMATIS_FLAC_E_CRC;
-    // decorrelate and store
-    const int64_t take = std::min<int64_t>(n, std::max<int64_t>(0, max_frames - done));
-    for (int64_t i = 0; i < take; ++i) {
-      int64_t a = sub[0][i], b = nch > 1 ? sub[1][i] : 0;
-      if (asg == 8) b = a - b;                 // left, side -> right
-      else if (asg == 9) a = a + b;            // side, right -> left
-      else if (asg == 10) {                    // mid, side
-        const int64_t m = (a << 1) | (b & 1);
-        a = (m + b) >> 1;
-        b = (m - b) >> 1;
-      }
-      int32_t* o = pcm + (done + i) * nch;
-      o[0] = (int32_t)a;
-      if (nch > 1) o[1] = (int32_t)b;
-      for (int c = 2; c < nch; ++c) o[c] = (int32_t)sub[c][i];
-    }
-    done += n;
-    p += fbytes + 2;
+  // frames are independent: byte ranges on host threads (thread 0 starts at
+  // the first frame, the others at the first verified frame in their range)
+  const size_t body = (size_t)len > p ? (size_t)len - p : 0;
+  int nt = (int)std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), 16);
+  if (const char* e = getenv("TOMATIS_FLAC_THREADS")) nt = std::max(1, atoi(e));
+  nt = (int)std::max<size_t>(1, std::min<size_t>(nt, body / (1u << 20)));
+  std::vector<int> rcs(nt);
+  std::vector<int64_t> ends(nt);
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t) {
+    const size_t lo = p + body * t / nt, hi = p + body * (t + 1) / nt;
+    if (t == nt - 1)
+      decode_range(d, (size_t)len, lo, (size_t)len, t == 0, ch0, bps0, nominal, pcm, max_frames,
+                   &rcs[t], &ends[t]);
+    else
+      th.emplace_back(decode_range, d, (size_t)len, lo, hi, t == 0, ch0, bps0, nominal, pcm,
+                      max_frames, &rcs[t], &ends[t]);
   }
+  for (auto& x : th) x.join();
+  int64_t done = 0;
+  for (int t = 0; t < nt; ++t) {
+    if (rcs[t]) return rcs[t];
+    done = std::max(done, ends[t]);
+  }
+  if (total) done = std::min(done, total);
   if (frames_out) *frames_out = std::min(done, max_frames);
   return TOMATIS_FLAC_OK;
 }

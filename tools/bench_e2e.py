@@ -68,7 +68,7 @@ def main():
         "e2e_host_to_host_msamples_s": round(S / (t_h2d + t_run + t_d2h), 1),
         "e2e_pinned_msamples_s": round(S / (t_h2d_pin + t_run + t_d2h_pin), 1),
         "flac_pcm24_encode_msamples_s_threads": round(m * ch / t_enc / 1e6, 1),
-        "flac_pcm24_decode_msamples_s_1thread": round(m * ch / t_dec / 1e6, 1),
+        "flac_pcm24_decode_msamples_s_threads": round(m * ch / t_dec / 1e6, 1),
         "flac_ratio": round(len(blob) / (m * ch * 3), 3),
     }
     print(json.dumps(out), flush=True)
