@@ -21,10 +21,19 @@ def main():
     x_host = ss0.x.cpu().numpy().reshape(n, ch)
     del ss0
     torch.cuda.synchronize()
+    engine.PINNED_STAGING = False
     t0 = time.perf_counter()
     ss = engine.StreamSet.from_arrays([x_host], sr)
     torch.cuda.synchronize()
     t_h2d = time.perf_counter() - t0
+    del ss
+    engine.PINNED_STAGING = True
+    t_stage = []
+    for _ in range(2):  # first call allocates the page-locked block, the second reuses it
+        t0 = time.perf_counter()
+        ss = engine.StreamSet.from_arrays([x_host], sr)
+        torch.cuda.synchronize()
+        t_stage.append(time.perf_counter() - t0)
     pipe = engine.GatePipeline(ss, gate_ui=50, n_fft=2048, hop=512)
     pipe.run()
     torch.cuda.synchronize()
@@ -32,9 +41,18 @@ def main():
     res = pipe.run()
     torch.cuda.synchronize()
     t_run = time.perf_counter() - t0
+    engine.PINNED_STAGING = False
     t0 = time.perf_counter()
     y = res.output(0)
     t_d2h = time.perf_counter() - t0
+    engine.PINNED_STAGING = True
+    t_ostage = []
+    for _ in range(2):
+        t0 = time.perf_counter()
+        y2 = res.output(0)
+        t_ostage.append(time.perf_counter() - t0)
+    assert np.array_equal(y2, y)
+    del y2
     # pinned-staging variant of the two copies
     pin = torch.empty(n * ch, dtype=torch.float32, pin_memory=True)
     pin.numpy()[:] = x_host.reshape(-1)
@@ -65,7 +83,10 @@ def main():
         "device_step_ms": round(t_run * 1e3, 2),
         "d2h_pageable_ms": round(t_d2h * 1e3, 1), "d2h_pageable_gbs": round(n * ch * 4 / t_d2h / 1e9, 1),
         "d2h_pinned_gbs": round(n * ch * 4 / t_d2h_pin / 1e9, 1),
+        "from_arrays_staged_ms": [round(t * 1e3, 1) for t in t_stage],
+        "output_staged_ms": [round(t * 1e3, 1) for t in t_ostage],
         "e2e_host_to_host_msamples_s": round(S / (t_h2d + t_run + t_d2h), 1),
+        "e2e_staged_msamples_s": round(S / (t_stage[1] + t_run + t_ostage[1]), 1),
         "e2e_pinned_msamples_s": round(S / (t_h2d_pin + t_run + t_d2h_pin), 1),
         "flac_pcm24_encode_msamples_s_threads": round(m * ch / t_enc / 1e6, 1),
         "flac_pcm24_decode_msamples_s_threads": round(m * ch / t_dec / 1e6, 1),
