@@ -796,12 +796,40 @@ __global__ __launch_bounds__(256) void k_limiter(float* __restrict__ y,
 
 __global__ __launch_bounds__(256) void k_absmax(const float* __restrict__ x, int64_t n,
                                                 uint32_t* __restrict__ out) {
-  float m = 0.f;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x)
-    m = fmaxf(m, fabsf(x[i]));
+  // scalar head up to 16-byte alignment, float4 body (4 independent loads in
+  // flight per thread per iteration), scalar tail
+  const int64_t head = std::min<int64_t>(n, (int64_t)((16 - ((uintptr_t)x & 15)) & 15) >> 2);
+  const int64_t nb = (n - head) >> 2;
+  const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x + head);
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  float m0 = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f;
+  if (tid < head) m0 = fabsf(x[tid]);
+  int64_t i = tid;
+  for (; i + 3 * stride < nb; i += 4 * stride) {
+    const float4 a = x4[i], b = x4[i + stride], c = x4[i + 2 * stride], d = x4[i + 3 * stride];
+    m0 = fmaxf(m0, fmaxf(fmaxf(fabsf(a.x), fabsf(a.y)), fmaxf(fabsf(a.z), fabsf(a.w))));
+    m1 = fmaxf(m1, fmaxf(fmaxf(fabsf(b.x), fabsf(b.y)), fmaxf(fabsf(b.z), fabsf(b.w))));
+    m2 = fmaxf(m2, fmaxf(fmaxf(fabsf(c.x), fabsf(c.y)), fmaxf(fabsf(c.z), fabsf(c.w))));
+    m3 = fmaxf(m3, fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fmaxf(fabsf(d.z), fabsf(d.w))));
+  }
+  for (; i < nb; i += stride) {
+    const float4 a = x4[i];
+    m0 = fmaxf(m0, fmaxf(fmaxf(fabsf(a.x), fabsf(a.y)), fmaxf(fabsf(a.z), fabsf(a.w))));
+  }
+  const int64_t t0 = head + nb * 4;
+  if (t0 + tid < n) m1 = fmaxf(m1, fabsf(x[t0 + tid]));
+  float m = fmaxf(fmaxf(m0, m1), fmaxf(m2, m3));
   m = wave_max(m);
-  if ((threadIdx.x & 63) == 0 && m > 0.f) atomicMax(out, __float_as_uint(m));
+  // one atomic per block: same-address atomics serialise in L2 (one per wave
+  // cost ~80 us for a 5-min stream)
+  __shared__ float wm[4];
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
+    if (m > 0.f) atomicMax(out, __float_as_uint(m));
+  }
 }
 
 __global__ __launch_bounds__(256) void k_scale_copy(const float* __restrict__ x,
@@ -1680,7 +1708,7 @@ int tomatis_apply_limiter(tomatis_plan_t p, float* y, const uint32_t* peaks, flo
 int tomatis_absmax(const float* x, int64_t n, uint32_t* out, void* hs) {
   if (!x || !out || n < 0) return TOMATIS_E_ARG;
   if (n == 0) return TOMATIS_OK;
-  const unsigned g = (unsigned)std::min<int64_t>(2048, (n + 1023) / 1024);
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(512, (n + 4095) / 4096));
   hipLaunchKernelGGL(k_absmax, dim3(g), dim3(256), 0, (hipStream_t)hs, x, n, out);
   return launch_check();
 }

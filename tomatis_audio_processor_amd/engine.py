@@ -131,6 +131,20 @@ class Plan:
             pass
 
 
+_POOL = None
+
+
+def _host_pool():
+    """Threads for per-stream host statistics (the box gives a GPU 16 CPUs)."""
+    global _POOL
+    if _POOL is None:
+        import concurrent.futures as cf
+        import os
+        n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        _POOL = cf.ThreadPoolExecutor(max_workers=max(1, min(16, n)))
+    return _POOL
+
+
 def _set_gate(st: TomatisStream, Ton: float, Toff: float):
     on, oe, off, fe = dsp.gate_bits(Ton, Toff)
     st.on_bits, st.off_bits = on, off
@@ -438,7 +452,8 @@ class AdaptivePipeline:
         r64 = self.r64.cpu().numpy() if F64 in prec else None
         lv = np.empty(self.plan.total_frames, np.float64)
         tlh = np.empty((ss.n_streams, 3), np.float64)
-        for i in range(ss.n_streams):
+
+        def stream_stats(i):  # numpy releases the GIL in log10 / partition
             a, F = sts[i].frame_base, sts[i].n_frames
             r = (r32 if prec[i] == F32 else r64)[a:a + F]
             lvi = dsp.r_to_level(r)
@@ -448,6 +463,11 @@ class AdaptivePipeline:
                 tlh[i] = (np.nan, np.nan, np.median(lvi) if F else 0.0)
             else:
                 tlh[i] = (np.percentile(valid, 5), np.percentile(valid, 95), np.median(valid))
+
+        if ss.n_streams > 1:
+            list(_host_pool().map(stream_stats, range(ss.n_streams)))
+        else:
+            stream_stats(0)
         self.levels.copy_(torch.from_numpy(lv))
         tl = torch.from_numpy(tlh.reshape(-1)).to(self.levels.device)
         self._tlh = tl
