@@ -156,3 +156,17 @@ def test_alpha_lattice_endpoints():
         for m in range(1, xf):
             a = a + 1.0 / xf
             assert lat[m] == a
+
+
+def test_level_stats_bit_identical_to_numpy():
+    """dsp.level_stats (one partition) == np.percentile 5/95 + np.median, bitwise."""
+    from tomatis_audio_processor_amd import dsp
+    rng = np.random.default_rng(3)
+    for t in range(3000):
+        n = int(rng.integers(1, 300)) if t % 2 else int(rng.integers(1, 20000))
+        v = rng.standard_normal(n) * 20 - 40
+        if t % 3 == 0:
+            v = np.round(v, 1)  # ties
+        got = np.array(dsp.level_stats(v))
+        ref = np.array([np.percentile(v, 5), np.percentile(v, 95), np.median(v)])
+        assert np.array_equal(got.view(np.uint64), ref.view(np.uint64)), (n, got, ref)

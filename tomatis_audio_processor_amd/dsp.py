@@ -289,3 +289,33 @@ def adaptive_frames(N: int, n_fft: int, hop: int):
     if len(ok) == 0:
         return 0, 0, 0
     return int(ok[0]), int(len(ok)), int(orig[ok[0]])
+
+
+def level_stats(valid: np.ndarray):
+    """``(np.percentile(v, 5), np.percentile(v, 95), np.median(v))`` of a
+    float64 array with one ``np.partition`` (numpy 2.x 'linear' rule and
+    median rule restated; src/process_tomatis_adaptive.py:129-131 calls the
+    three separately, each partitioning again).  Bit-identical: checked
+    against the numpy calls in tests/test_host_logic.py."""
+    v = np.asarray(valid, np.float64)
+    n = v.size
+    q = np.array([5.0, 95.0]) / 100
+    vi = (n - 1) * q
+    prev = np.floor(vi)
+    above = vi >= n - 1
+    pi = np.where(above, n - 1, prev).astype(np.intp)
+    ni = np.where(above, n - 1, prev + 1).astype(np.intp)
+    gamma = np.where(above, 0.0, vi - prev)
+    h = n // 2
+    mk = [h - 1, h] if n % 2 == 0 else [h]
+    kth = np.unique(np.concatenate([pi, ni, mk, [0, n - 1]]))
+    part = np.partition(v, kth)
+    a, b = part[pi], part[ni]
+    d = b - a
+    lerp = a + d * gamma
+    lerp = np.where(gamma >= 0.5, b - d * (1 - gamma), lerp)
+    if n % 2:
+        med = part[h] + 0.0
+    else:
+        med = (0.0 + part[h - 1] + part[h]) / 2.0
+    return float(lerp[0]), float(lerp[1]), float(med)

@@ -450,19 +450,30 @@ class AdaptivePipeline:
             check(L.tomatis_levels(P, ptr(ss.x), ptr(self.r64), F64, hs), "levels f64")
         r32 = self.r32.cpu().numpy() if F32 in prec else None
         r64 = self.r64.cpu().numpy() if F64 in prec else None
-        lv = np.empty(self.plan.total_frames, np.float64)
+        # levels of every frame in one elementwise call per precision (identical
+        # to the reference's per-frame calls), then per-stream statistics
+        lv32 = dsp.r_to_level(r32) if r32 is not None else None
+        lv64 = dsp.r_to_level(r64) if r64 is not None else None
+        if lv64 is None:
+            lv = lv32
+        elif lv32 is None:
+            lv = lv64
+        else:
+            lv = np.empty(self.plan.total_frames, np.float64)
+            for i in range(ss.n_streams):
+                a, F = sts[i].frame_base, sts[i].n_frames
+                lv[a:a + F] = (lv32 if prec[i] == F32 else lv64)[a:a + F]
+        lv = np.ascontiguousarray(lv[:self.plan.total_frames], np.float64)
         tlh = np.empty((ss.n_streams, 3), np.float64)
 
-        def stream_stats(i):  # numpy releases the GIL in log10 / partition
+        def stream_stats(i):  # numpy releases the GIL in partition
             a, F = sts[i].frame_base, sts[i].n_frames
-            r = (r32 if prec[i] == F32 else r64)[a:a + F]
-            lvi = dsp.r_to_level(r)
-            lv[a:a + F] = lvi
+            lvi = lv[a:a + F]
             valid = lvi[lvi > -70]
             if len(valid) == 0:
                 tlh[i] = (np.nan, np.nan, np.median(lvi) if F else 0.0)
             else:
-                tlh[i] = (np.percentile(valid, 5), np.percentile(valid, 95), np.median(valid))
+                tlh[i] = dsp.level_stats(valid)
 
         if ss.n_streams > 1:
             list(_host_pool().map(stream_stats, range(ss.n_streams)))
