@@ -180,3 +180,25 @@ def test_fused_limiter_matches_two_pass(monkeypatch):
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
     assert np.count_nonzero(outs[0][1].view(np.float32) > 0.999) > 10
     np.testing.assert_array_equal(outs[0][0].view(np.uint32), outs[1][0].view(np.uint32))
+
+
+@pytest.mark.parametrize("xfade_ms", [0.0, 500.0, 5000.0])
+def test_adaptive_alpha_long_streams(xfade_ms):
+    """Chunk-parallel adaptive alpha (k_minhold) == the sequential reference scan
+    (process_tomatis_adaptive.py:253-265) bit-for-bit on streams long enough for
+    many 256-frame chunks; 5000 ms makes most chunks sync-free (carry chain)."""
+    torch, E = _engine()
+    from oracle import tomatis_oracle as orc
+    ss = E.StreamSet.synthetic(3, 44100 * 95 + 777, 2, 44100, seed0=71)
+    pipe = E.AdaptivePipeline(ss, n_fft=2048, hop=512, xfade_ms=xfade_ms)
+    res = pipe.run()
+    torch.cuda.synchronize()
+    for i in range(3):
+        st = res.stream_states(i)
+        assert len(st) > 8 * 256
+        ref = orc.alpha_scan_adaptive(st, pipe.xf)
+        got = res.stream_alpha(i)
+        assert np.array_equal(got.view(np.uint64), ref.view(np.uint64))
+        a, F = res.frame_base[i], res.n_frames[i]
+        rows = pipe.rows[a:a + F].cpu().numpy().astype(np.int64)
+        assert np.array_equal(rows, 2 + np.rint(ref * max(pipe.xf, 1)).astype(np.int64))

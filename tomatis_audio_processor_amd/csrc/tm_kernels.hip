@@ -637,6 +637,7 @@ __global__ void k_alpha_xfade(const TomatisStream* __restrict__ st, int n_stream
 // Adaptive: min-hold gate, bisection, final states, alpha (one block per stream)
 // state id = (C - 1) * (mh + 1) + min(since, mh)
 // ===========================================================================
+constexpr int kMhAlphaChunks = 2048;  // alpha chunks per stream (LDS carries)
 __device__ __forceinline__ int mh_step(int id, double lv, double ton, double toff, int mh) {
   const int c2 = id / (mh + 1);
   int since = id - c2 * (mh + 1);
@@ -754,16 +755,79 @@ __global__ __launch_bounds__(1024) void k_minhold(const double* __restrict__ lev
     }
   }
   __syncthreads();
-  // alpha (process_tomatis_adaptive.py:253-265), sequential
-  if (threadIdx.x == 0 && F > 0) {
+  // alpha (process_tomatis_adaptive.py:253-265): a_0 = target(s_0), then
+  // a_k = step(a_{k-1}, target(s_k)).  Segment-parallel and exact, as the xfade
+  // alpha: after J = xf + 2 equal states alpha equals the target exactly (and
+  // a_0 is exact), so every chunk computes from its first such "sync" frame on;
+  // one thread chains the chunk carries; the prefixes follow from the carries.
+  if (F > 0) {
     const double step = xf > 0 ? 1.0 / xf : 1.0;
     const int xfe = xf > 0 ? xf : 1;
-    double a = states[S.frame_base] == 2 ? 1.0 : 0.0;
-    for (int64_t k = 0; k < F; ++k) {
+    const int J = xf + 2;
+    const uint8_t* stt = states + S.frame_base;
+    const int64_t CHK = max<int64_t>(256, (F + kMhAlphaChunks - 1) / kMhAlphaChunks);
+    const int nch = (int)((F + CHK - 1) / CHK);
+    __shared__ int32_t a_q[kMhAlphaChunks];
+    __shared__ double a_fin[kMhAlphaChunks], a_carry[kMhAlphaChunks];
+    auto put = [&](int64_t k, double a) {
       const int64_t f = S.frame_base + k;
-      if (k > 0) a = alpha_step(a, states[f] == 2 ? 1.0 : 0.0, step);
       if (alpha) alpha[f] = a;
       if (rows) rows[f] = (uint16_t)(2 + (int)rint(a * xfe));
+    };
+    for (int c = threadIdx.x; c < nch; c += blockDim.x) {
+      const int64_t k0 = c * CHK;
+      const int nf = (int)min<int64_t>(CHK, F - k0);
+      int q = 0;
+      if (k0 > 0) {
+        uint8_t prev = stt[k0 - 1];
+        int run = 1;
+        int64_t k = k0 - 2;
+        for (; k >= 0 && run < J && stt[k] == prev; --k) ++run;
+        if (k < 0) run = J;  // equal back to frame 0, whose alpha is exact
+        q = nf;
+        for (int j = 0; j < nf; ++j) {
+          const uint8_t t = stt[k0 + j];
+          run = (t == prev) ? min(run + 1, J) : 1;
+          prev = t;
+          if (xf == 0 || run >= J) {
+            q = j;
+            break;
+          }
+        }
+      }
+      a_q[c] = q;
+      if (q < nf) {
+        double a = stt[k0 + q] == 2 ? 1.0 : 0.0;
+        put(k0 + q, a);
+        for (int j = q + 1; j < nf; ++j) {
+          a = alpha_step(a, stt[k0 + j] == 2 ? 1.0 : 0.0, step);
+          put(k0 + j, a);
+        }
+        a_fin[c] = a;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double cur = 0.0;
+      for (int c = 0; c < nch; ++c) {
+        a_carry[c] = cur;
+        const int64_t k0 = c * CHK;
+        const int nf = (int)min<int64_t>(CHK, F - k0);
+        if (a_q[c] < nf) {
+          cur = a_fin[c];
+        } else {
+          for (int j = 0; j < nf; ++j) cur = alpha_step(cur, stt[k0 + j] == 2 ? 1.0 : 0.0, step);
+        }
+      }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < nch; c += blockDim.x) {
+      const int64_t k0 = c * CHK;
+      double a = a_carry[c];
+      for (int j = 0; j < a_q[c]; ++j) {
+        a = alpha_step(a, stt[k0 + j] == 2 ? 1.0 : 0.0, step);
+        put(k0 + j, a);
+      }
     }
   }
   (void)alpha_adaptive;
