@@ -50,9 +50,6 @@ namespace {
 
 constexpr int kT = 256;                // threads per spectrum workgroup
 constexpr int kMaxN = 8192;            // largest n_fft
-constexpr int kMaxU2 = kMaxN / 2 / kT; // radix-2 butterflies per thread (16)
-constexpr int kMaxU4 = kMaxN / 4 / kT; // radix-4 butterflies per thread (8)
-constexpr int kMaxUB = kMaxN / 2 / kT + 1;  // bins per thread (17)
 constexpr float kEps = 1e-12f;
 
 int an_fail(hipError_t e) { return e == hipSuccess ? TOMATIS_OK : TOMATIS_E_HIP; }
@@ -211,10 +208,15 @@ __device__ __forceinline__ float2 cmul(float2 a, float2 w) {
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
 
-__device__ void lds_fft(float2* __restrict__ buf, int n, int logn, const float2* __restrict__ tw) {
+template <int N>
+__device__ __forceinline__ void lds_fft(float2* __restrict__ buf, const float2* __restrict__ tw) {
+  constexpr int n = N;
+  constexpr int logn = __builtin_ctz(N);
+  constexpr int kMaxU2 = (N / 2 + kT - 1) / kT;  // radix-2 butterflies per thread
+  constexpr int kMaxU4 = (N / 4 + kT - 1) / kT;  // radix-4 butterflies per thread
   const int t = threadIdx.x;
   int Ns = 1;
-  if (logn & 1) {  // radix-2 stage at Ns = 1: out[2j + q] = a +- b
+  if constexpr (logn & 1) {  // radix-2 stage at Ns = 1: out[2j + q] = a +- b
     const int h = n >> 1;
     float2 o0[kMaxU2], o1[kMaxU2];
 #pragma unroll
@@ -298,12 +300,12 @@ __device__ __forceinline__ float sig_at(const float* __restrict__ x, int64_t p, 
 }
 
 // MAG / LOGPOW: workgroup per frame pair (2g, 2g+1) packed as a + ib
-template <int KIND, int SIG>
+template <int KIND, int SIG, int N>
 __global__ __launch_bounds__(kT) void k_an_spec_pair(SpecArgs A) {
-  extern __shared__ float2 buf[];
+  __shared__ float2 buf[N];
   const int f0 = blockIdx.x * 2, f1 = f0 + 1;
   const bool has1 = f1 < A.n_frames;
-  const int n = A.n_fft;
+  constexpr int n = N;
   const int64_t p0 = (int64_t)f0 * A.hop, p1 = (int64_t)f1 * A.hop;
   for (int i = threadIdx.x; i < n; i += kT) {
     const float w = A.win[i];
@@ -312,7 +314,7 @@ __global__ __launch_bounds__(kT) void k_an_spec_pair(SpecArgs A) {
     buf[i] = make_float2(a, b);
   }
   __syncthreads();
-  lds_fft(buf, n, A.logn, A.tw);
+  lds_fft<N>(buf, A.tw);
   float* o0 = A.out + (int64_t)f0 * A.n_bins;
   float* o1 = A.out + (int64_t)f1 * A.n_bins;
   for (int k = threadIdx.x; k < A.n_bins; k += kT) {
@@ -335,11 +337,12 @@ __global__ __launch_bounds__(kT) void k_an_spec_pair(SpecArgs A) {
 }
 
 // RATIO: workgroup per frame; per channel one FFT of x_c + i y_c
-template <int CH>
+template <int CH, int N>
 __global__ __launch_bounds__(kT) void k_an_spec_ratio(SpecArgs A) {
-  extern __shared__ float2 buf[];
+  __shared__ float2 buf[N];
+  constexpr int kMaxUB = (N / 2 + 1 + kT - 1) / kT;  // bins per thread
   const int f = blockIdx.x;
-  const int n = A.n_fft;
+  constexpr int n = N;
   const int64_t p0 = (int64_t)f * A.hop;
   float ax[kMaxUB], ay[kMaxUB];
 #pragma unroll
@@ -352,7 +355,7 @@ __global__ __launch_bounds__(kT) void k_an_spec_ratio(SpecArgs A) {
       buf[i] = make_float2(A.x[q] * w, A.y[q] * w);
     }
     __syncthreads();
-    lds_fft(buf, n, A.logn, A.tw);
+    lds_fft<N>(buf, A.tw);
 #pragma unroll
     for (int u = 0; u < kMaxUB; ++u) {
       const int k = threadIdx.x + u * kT;
@@ -581,15 +584,17 @@ int tomatis_an_spectra(const float* x, const float* y, int64_t n, int32_t ch, in
   SpecArgs A{x, y, win, nullptr, out, n_fft, logn, hop, (int)F, n_fft / 2 + 1, scale};
   int rc = twiddles(n_fft, s, &A.tw);
   if (rc != TOMATIS_OK) return rc;
-  const size_t lds = sizeof(float2) * n_fft;
   if (kind == TOMATIS_AN_RATIO) {
     if (!y) return TOMATIS_E_ARG;
-    if (ch == 1)
-      hipLaunchKernelGGL(k_an_spec_ratio<1>, dim3((unsigned)F), dim3(kT), lds, s, A);
-    else if (ch == 2)
-      hipLaunchKernelGGL(k_an_spec_ratio<2>, dim3((unsigned)F), dim3(kT), lds, s, A);
-    else
-      return TOMATIS_E_UNSUPPORTED;
+    if (ch != 1 && ch != 2) return TOMATIS_E_UNSUPPORTED;
+    const dim3 g((unsigned)F);
+#define AN_RATIO(NN)                                                                 \
+  if (n_fft == NN) {                                                                 \
+    if (ch == 1) hipLaunchKernelGGL((k_an_spec_ratio<1, NN>), g, dim3(kT), 0, s, A); \
+    else hipLaunchKernelGGL((k_an_spec_ratio<2, NN>), g, dim3(kT), 0, s, A);         \
+  }
+    AN_RATIO(256) AN_RATIO(512) AN_RATIO(1024) AN_RATIO(2048) AN_RATIO(4096) AN_RATIO(8192)
+#undef AN_RATIO
     return an_launch();
   }
   if (kind != TOMATIS_AN_MAG && kind != TOMATIS_AN_LOGPOW) return TOMATIS_E_ARG;
@@ -601,13 +606,17 @@ int tomatis_an_spectra(const float* x, const float* y, int64_t n, int32_t ch, in
     return TOMATIS_E_ARG;
   }
   const dim3 g((unsigned)((F + 1) / 2));
-#define AN_PAIR(K, S)                                                                  \
-  if (kind == K && sig_mode == S) hipLaunchKernelGGL((k_an_spec_pair<K, S>), g, dim3(kT), lds, s, A);
+#define AN_PAIR_N(K, S, NN) \
+  if (kind == K && sig_mode == S && n_fft == NN) hipLaunchKernelGGL((k_an_spec_pair<K, S, NN>), g, dim3(kT), 0, s, A);
+#define AN_PAIR(K, S) \
+  AN_PAIR_N(K, S, 256) AN_PAIR_N(K, S, 512) AN_PAIR_N(K, S, 1024) AN_PAIR_N(K, S, 2048) \
+  AN_PAIR_N(K, S, 4096) AN_PAIR_N(K, S, 8192)
   AN_PAIR(TOMATIS_AN_MAG, TOMATIS_AN_SIG_RAW)
   AN_PAIR(TOMATIS_AN_MAG, TOMATIS_AN_SIG_POWER_MONO)
   AN_PAIR(TOMATIS_AN_LOGPOW, TOMATIS_AN_SIG_RAW)
   AN_PAIR(TOMATIS_AN_LOGPOW, TOMATIS_AN_SIG_POWER_MONO)
 #undef AN_PAIR
+#undef AN_PAIR_N
   return an_launch();
 }
 
