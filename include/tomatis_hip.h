@@ -213,6 +213,12 @@ int tomatis_plan_error(tomatis_plan_t plan, void* hip_stream);
 /* max |x| over n floats as float bits (out zeroed by caller). */
 int tomatis_absmax(const float* x, int64_t n, uint32_t* out_bits, void* hip_stream);
 
+/* max |x| of every stream of the plan (stream table in_off / n * ch), one
+ * launch: out_bits[s] as float bits (zeroed by caller).  Replaces the per-file
+ * np.max(np.abs(x)) of src/process_tomatis_adaptive.py:201 for a batch. */
+int tomatis_absmax_streams(tomatis_plan_t plan, const float* x, uint32_t* out_bits,
+                           void* hip_stream);
+
 /* y[i] = x[i] * scale (float32), n floats (layer-2 gain-protect copy). */
 int tomatis_scale_copy(const float* x, float* y, int64_t n, float scale, void* hip_stream);
 

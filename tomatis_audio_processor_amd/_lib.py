@@ -75,6 +75,7 @@ _SIGS = {
     "tomatis_stft_ola_limited": (C.c_int, [_P, _P, _P, C.c_int32, _P, _P, _P, C.c_float, _P]),
     "tomatis_plan_error": (C.c_int, [_P, _P]),
     "tomatis_absmax": (C.c_int, [_P, C.c_int64, _P, _P]),
+    "tomatis_absmax_streams": (C.c_int, [_P, _P, _P, _P]),
     "tomatis_scale_copy": (C.c_int, [_P, _P, C.c_int64, C.c_float, _P]),
     "tomatis_synth_fill": (C.c_int, [_P, C.c_int64, C.c_int32, C.c_int32, C.c_uint32,
                                      C.c_int64, _P]),

@@ -858,15 +858,14 @@ __global__ __launch_bounds__(256) void k_limiter(float* __restrict__ y,
     base[i] = base[i] * sc;
 }
 
-__global__ __launch_bounds__(256) void k_absmax(const float* __restrict__ x, int64_t n,
-                                                uint32_t* __restrict__ out) {
+__device__ __forceinline__ void absmax_body(const float* __restrict__ x, int64_t n,
+                                            uint32_t* __restrict__ out, int64_t tid,
+                                            int64_t stride) {
   // scalar head up to 16-byte alignment, float4 body (4 independent loads in
   // flight per thread per iteration), scalar tail
   const int64_t head = std::min<int64_t>(n, (int64_t)((16 - ((uintptr_t)x & 15)) & 15) >> 2);
   const int64_t nb = (n - head) >> 2;
   const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x + head);
-  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   float m0 = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f;
   if (tid < head) m0 = fabsf(x[tid]);
   int64_t i = tid;
@@ -894,6 +893,19 @@ __global__ __launch_bounds__(256) void k_absmax(const float* __restrict__ x, int
     m = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
     if (m > 0.f) atomicMax(out, __float_as_uint(m));
   }
+}
+__global__ __launch_bounds__(256) void k_absmax(const float* __restrict__ x, int64_t n,
+                                                uint32_t* __restrict__ out) {
+  absmax_body(x, n, out, (int64_t)blockIdx.x * blockDim.x + threadIdx.x,
+              (int64_t)gridDim.x * blockDim.x);
+}
+// every stream of a plan in one launch: blockIdx.y = stream
+__global__ __launch_bounds__(256) void k_absmax_streams(const float* __restrict__ x,
+                                                        const TomatisStream* __restrict__ st,
+                                                        int ch, uint32_t* __restrict__ out) {
+  const TomatisStream S = st[blockIdx.y];
+  absmax_body(x + S.in_off, S.n * ch, out + blockIdx.y,
+              (int64_t)blockIdx.x * blockDim.x + threadIdx.x, (int64_t)gridDim.x * blockDim.x);
 }
 
 __global__ __launch_bounds__(256) void k_scale_copy(const float* __restrict__ x,
@@ -1774,6 +1786,19 @@ int tomatis_absmax(const float* x, int64_t n, uint32_t* out, void* hs) {
   if (n == 0) return TOMATIS_OK;
   const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(512, (n + 4095) / 4096));
   hipLaunchKernelGGL(k_absmax, dim3(g), dim3(256), 0, (hipStream_t)hs, x, n, out);
+  return launch_check();
+}
+
+int tomatis_absmax_streams(tomatis_plan_t p, const float* x, uint32_t* out, void* hs) {
+  if (!p || !x || !out) return TOMATIS_E_ARG;
+  if (p->n_streams == 0) return TOMATIS_OK;
+  int64_t nmax = 0;
+  for (const auto& S : p->hs) nmax = std::max<int64_t>(nmax, S.n * p->d.ch);
+  if (nmax == 0) return TOMATIS_OK;
+  const unsigned gx = (unsigned)std::max<int64_t>(
+      1, std::min<int64_t>(std::max(8, 1024 / p->n_streams), (nmax + 4095) / 4096));
+  hipLaunchKernelGGL(k_absmax_streams, dim3(gx, p->n_streams), dim3(256), 0, (hipStream_t)hs, x,
+                     p->st, p->d.ch, out);
   return launch_check();
 }
 

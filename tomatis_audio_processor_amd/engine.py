@@ -425,10 +425,7 @@ class AdaptivePipeline:
         sts = self.plan.streams
         # 1. input peak per stream -> attenuation (process_tomatis_adaptive.py:201-215)
         self.inpk.zero_()
-        for i in range(ss.n_streams):
-            n = ss.lens[i] * ss.ch
-            sub = ss.x[ss.offs[i]:ss.offs[i] + n]
-            check(L.tomatis_absmax(ptr(sub), n, ptr(self.inpk[i:i + 1]), hs), "absmax")
+        check(L.tomatis_absmax_streams(P, ptr(ss.x), ptr(self.inpk), hs), "absmax_streams")
         pk = self.inpk.cpu().numpy().astype(np.uint32).view(np.float32)
         self.atten, prec = [], []
         for i in range(ss.n_streams):
