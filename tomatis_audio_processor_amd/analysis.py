@@ -178,7 +178,13 @@ def stft_logpower_median(x_lr, sr: int, n_fft: int, hop: int, music_dbfs: float)
 def find_stable_frames(states, margin=2):
     """validate_layer1.find_stable_frames: indices whose +-margin window is all
     C1 (first list) or all C2 (second list)."""
-    s = np.asarray([1 if v == "C1" else (2 if v == "C2" else 0) for v in states], np.int8)
+    a = np.asarray(states)
+    if a.dtype.kind in "US":  # vectorised for the usual list of "C1"/"C2" strings
+        s = np.zeros(len(a), np.int8)
+        s[a == "C1"] = 1
+        s[a == "C2"] = 2
+    else:
+        s = np.asarray([1 if v == "C1" else (2 if v == "C2" else 0) for v in states], np.int8)
     n = len(s)
     c1, c2 = [], []
     if n - 2 * margin <= 0:
