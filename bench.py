@@ -240,7 +240,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "k_stft_ola (fused frame/window/FFT/gain/IFFT/OLA/normalise)",
+                         "kernel": "k_stft_ola (fused frame/window/FFT/gain/IFFT/OLA/normalise + per-chunk limiter)",
                          "kernel_ms": round(kern_ms, 4),
                          "alg_bytes_per_launch": alg_bytes},
             "compute": {"bound": "valu-fp32", "achieved": round(tflops, 2),
