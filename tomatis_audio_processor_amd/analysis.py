@@ -175,26 +175,34 @@ def stft_logpower_median(x_lr, sr: int, n_fft: int, hop: int, music_dbfs: float)
     return freqs, med.cpu().numpy(), used
 
 
+def _stable_classes(states, margin=2):
+    """int8 per state index: 1 = stable C1, 2 = stable C2, 0 = neither
+    (validate_layer1.find_stable_frames' rule, vectorised)."""
+    s = None
+    try:  # fast path: a list of "C1"/"C2" strings joined into one byte buffer
+        b = np.frombuffer("".join(states).encode("ascii"), np.uint8)
+        if b.size == 2 * len(states) and np.all(b[0::2] == ord("C")):
+            d = b[1::2]
+            s = np.where(d == ord("1"), 1, np.where(d == ord("2"), 2, 0)).astype(np.int8)
+    except (TypeError, UnicodeEncodeError):
+        s = None
+    if s is None:
+        s = np.asarray([1 if v == "C1" else (2 if v == "C2" else 0) for v in states], np.int8)
+    n = len(s)
+    cls = np.zeros(n, np.int8)
+    if n - 2 * margin <= 0:
+        return cls
+    win = np.lib.stride_tricks.sliding_window_view(s, 2 * margin + 1)  # starts at i - margin
+    cls[margin:n - margin][np.all(win == 1, axis=1)] = 1
+    cls[margin:n - margin][np.all(win == 2, axis=1)] = 2
+    return cls
+
+
 def find_stable_frames(states, margin=2):
     """validate_layer1.find_stable_frames: indices whose +-margin window is all
     C1 (first list) or all C2 (second list)."""
-    a = np.asarray(states)
-    if a.dtype.kind in "US":  # vectorised for the usual list of "C1"/"C2" strings
-        s = np.zeros(len(a), np.int8)
-        s[a == "C1"] = 1
-        s[a == "C2"] = 2
-    else:
-        s = np.asarray([1 if v == "C1" else (2 if v == "C2" else 0) for v in states], np.int8)
-    n = len(s)
-    c1, c2 = [], []
-    if n - 2 * margin <= 0:
-        return c1, c2
-    w = 2 * margin + 1
-    win = np.lib.stride_tricks.sliding_window_view(s, w)  # window i starts at i - margin
-    all1 = np.all(win == 1, axis=1)
-    all2 = np.all(win == 2, axis=1)
-    idx = np.arange(margin, n - margin)
-    return idx[all1].tolist(), idx[all2].tolist()
+    cls = _stable_classes(states, margin)
+    return np.nonzero(cls == 1)[0].tolist(), np.nonzero(cls == 2)[0].tolist()
 
 
 def compute_conditional_spectrum(x, y, sr, states, n_fft, hop, level_threshold=-60):
@@ -217,11 +225,9 @@ def compute_conditional_spectrum(x, y, sr, states, n_fft, hop, level_threshold=-
     freqs = np.fft.rfftfreq(n_fft, 1 / sr)
     nb = len(freqs)
     F = max(0, _n_frames(n, n_fft, hop))  # frames idx with idx*hop + n_fft <= len(x)
-    c1_stable, c2_stable = find_stable_frames(states, margin=2)
     cls = np.zeros(F, np.int8)
-    for lst, v in ((c1_stable, 1), (c2_stable, 2)):
-        ids = np.asarray(lst, np.int64)
-        cls[ids[ids < F]] = v
+    sc = _stable_classes(states, margin=2)[:F]
+    cls[:len(sc)] = sc
     out = []
     if F > 0:
         r = _frame_r(xd, n, ch, n_fft, hop, AN_LEVEL_CHMEAN)
