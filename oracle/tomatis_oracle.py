@@ -35,7 +35,6 @@ The OLA itself is kept as a frame-ordered loop (float32 sum order matters).
 """
 from __future__ import annotations
 
-import math
 
 import numpy as np
 from numpy.lib.stride_tricks import as_strided
@@ -582,7 +581,6 @@ def ceil_div(a, b):
 
 
 __all__ = [n for n in dir() if not n.startswith("_")] + ["_std_schedule"]
-_unused = math  # keep import for downstream users of math-based helpers
 
 
 # ----------------------------------------------------------------------------

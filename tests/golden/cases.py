@@ -1,7 +1,8 @@
 """Golden-fixture case table (shared by tools/make_goldens.py and the tests).
 
 Every case is a seeded synthetic input (``tomatis_audio_processor_amd.synth``)
-plus reference parameters.  ``bypass`` marks configurations outside the
+plus reference parameters (``in_scale`` scales it, ``silence`` zeroes that many
+samples at both ends).  ``bypass`` marks configurations outside the
 reference's 48 kHz-stereo guard, run through the guard bypass.
 Lengths are chosen so that standard-mode cases cover every tail residue class
 that matters (N - n_fft mod hop = 0, 9, 259, 777) and at least one case spans
@@ -34,6 +35,11 @@ CASES = [
          seed=7, params=dict(gate_ui=50, n_fft=2048, hop=300)),
     dict(name="std_48k_st_short", mode="standard", sr=S48, ch=2, N=3000,
          seed=8, params=dict(gate_ui=0, n_fft=2048, hop=512)),
+    # tail class where the reference's last-chunk limiter scale is set by an
+    # ill-conditioned tail sample (sum w^2 < 1e-3; SURVEY F7, process_tomatis.py:447-453):
+    # found by tools/find_tail_cases.py (1 of 440 lengths near 250 k)
+    dict(name="std_48k_st_tail_ill", mode="standard", sr=S48, ch=2, N=250875,
+         seed=2, params=dict(gate_ui=50, n_fft=2048, hop=512)),
     # --- xfade (src/process_tomatis_xfade.py) ------------------------------
     dict(name="xfade_48k_st_2048_512_500ms", mode="xfade", sr=S48, ch=2,
          N=288000 + 5000, seed=11,
@@ -59,6 +65,11 @@ CASES = [
     dict(name="l2_48k_st_nopad_gain", mode="layer2", sr=S48, ch=2, N=100000,
          seed=32, params=dict(pad=False, global_gain_db=-6.0,
                               auto_gain_protect=False)),
+    # gain protect set by a well-conditioned sample: digital silence at both
+    # ends keeps the ill-conditioned head/tail samples exactly 0, so peak_seen
+    # (layer2_apply_eq.py:177,213) and the _gp scale are determined
+    dict(name="l2_48k_st_pad_gp_silent_edges", mode="layer2", sr=S48, ch=2, N=150000,
+         seed=33, silence=4096, params=dict(n_fft=2048, hop=512, global_gain_db=12.0)),
     # --- layer 2b (src/layer2b_apply_residual_eq*.py) -----------------------
     dict(name="l2b_96k_st_4096_1024", mode="layer2b", sr=S96, ch=2,
          N=96000 * 2 + 1500, seed=41, params=dict(n_fft=4096, hop=1024)),

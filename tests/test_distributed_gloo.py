@@ -24,7 +24,7 @@ def _worker(rank, ws, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     costs = [14_400_000 * 2] * 509 + [1000, 2000, 3000]
     mine = sharding.lpt_partition(costs, ws)[rank]
-    rec = np.array([[i, rank, 28124, 14000 + i, 7, 18, 18, 0x3F7FBE77] for i in mine],
+    rec = np.array([[i, rank, 28124, 14000 + i, 7, 18, 18, 0x3F7FBE77, 0] for i in mine],
                    np.int64).reshape(-1, sharding.REC)
     allr = sharding.gather_manifest(rec)
     q.put((rank, len(mine), allr.shape, allr[:, 0].tolist()))

@@ -1,0 +1,144 @@
+"""GPU: compositions of the per-mode pipelines against the oracle.
+
+* C5 chain (BASELINE.json configs[4]): xfade 500 ms -> layer-2b residual EQ at
+  96 kHz, 4096/1024, stage 2 reading stage 1's device buffer exactly as
+  ``bench.ChainC5`` hands it off.  Stage 1 vs ``orc.process_standard``;
+  stage 2 vs ``orc.apply_residual_eq`` on the GPU's own float stage-1 output;
+  the chain end to end vs the oracle chain.
+* C3-shaped adaptive batch (configs[2]): 8 streams of mixed loudness in ONE
+  plan, so the float32 (loud) and float64 (quiet) precision paths
+  share one levels pass pair and one ``k_minhold`` bisection launch; per
+  stream threshold, states, alpha and samples vs ``orc.process_adaptive``.
+"""
+import numpy as np
+import pytest
+
+from oracle import tomatis_oracle as orc
+from tomatis_audio_processor_amd.synth import synth_stream
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+TAU = 1e-3
+
+
+def _engine():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from tomatis_audio_processor_amd import engine
+    return torch, engine
+
+
+def test_c5_chain_xfade_then_layer2b():
+    torch, E = _engine()
+    import bench
+    sr, n_fft, hop = 96000, 4096, 1024
+    lens = [sr * 10 + 333, sr * 7 + 1777, sr * 12 + 5000]
+    xs = [synth_stream(500 + i, n, 2, sr) for i, n in enumerate(lens)]
+    ss = E.StreamSet.from_arrays(xs, sr)
+    chain = bench.ChainC5(E, ss, sr, n_fft, hop)
+    res2 = chain.run()
+    torch.cuda.synchronize()
+    res1 = chain.s1.result()
+    chain.s1.plan.check_device()
+    rf = np.geomspace(20.0, sr / 2, 400)
+    rd = 4.0 * np.sin(np.log2(rf / 20.0) * 1.7) * np.exp(-rf / 12000.0)
+    for i, x in enumerate(xs):
+        N = lens[i]
+        # stage 1: xfade vs the oracle (scales determined: unflagged)
+        r1 = orc.process_standard(x, sr, gate_ui=50, gate_offset=-90, n_fft=n_fft, hop=hop,
+                                  xfade_ms=500.0)
+        y1 = res1.output(i)
+        assert not any(res1.scale_flags(i))
+        np.testing.assert_array_equal(res1.stream_states(i), r1["states"])
+        np.testing.assert_array_equal(res1.stream_alpha(i), r1["alpha"])
+        m1 = r1["wsum"][r1["pad"]:r1["pad"] + N] >= TAU
+        assert np.abs(y1[m1] - r1["y"][m1]).max() <= TOL
+        # stage 2 in isolation: oracle layer-2b on the GPU's own stage-1 floats
+        y2 = res2.output(i)
+        r2 = orc.apply_residual_eq(y1, sr, rf, rd, n_fft=n_fft, hop=hop)
+        assert y2.shape == r2["y"].shape
+        m2 = r2["wsum"] >= TAU
+        assert np.abs(y2[m2] - r2["y"][m2]).max() <= TOL
+        # end to end vs the oracle chain.  Stage-1 samples with sum w^2 < tau
+        # (its tail) are the reference's own rounding noise amplified (F7);
+        # every stage-2 frame that reads one is excluded, as are stage 2's own
+        # ill-conditioned samples.  Bound: stage-1 error (<= 1e-4) through a
+        # gain of at most +6 dB (x2, build_eq_from_residual's clamp) plus
+        # stage 2's own 1e-4.
+        rc = orc.apply_residual_eq(r1["y"], sr, rf, rd, n_fft=n_fft, hop=hop)
+        first_ill = int(np.argmin(m1)) if not m1.all() else N
+        k_bad = max(0, (first_ill - n_fft) // hop + 1)
+        m3 = m2.copy()
+        m3[k_bad * hop:] = False
+        assert m3.sum() > 0.9 * len(m3)
+        assert np.abs(y2[m3] - rc["y"][m3]).max() <= 3 * TOL
+
+
+def test_c3_mixed_loudness_batch():
+    torch, E = _engine()
+    sr, n_fft, hop = 44100, 2048, 512
+    scales = [1.0, 0.01, 1.0, 0.02, 3.0, 0.005, 1.0, 0.01]   # f32 / f64 paths interleaved
+    lens = [sr * 5 + 17 * i * i for i in range(8)]
+    xs = []
+    for i, (s, n) in enumerate(zip(scales, lens)):
+        x = synth_stream(700 + i, n, 2, sr)
+        xs.append(np.clip(x * np.float32(s), -1, 1).astype(np.float32) if s != 1.0 else x)
+    ss = E.StreamSet.from_arrays(xs, sr)
+    pipe = E.AdaptivePipeline(ss, n_fft=n_fft, hop=hop)
+    res = pipe.run()
+    torch.cuda.synchronize()
+    pipe.plan.check_device()
+    prec = res.extra["prec"]
+    assert len(set(prec)) == 2, "both precision paths must be in the batch"
+    thr = res.extra["thresholds"].cpu().numpy()
+    for i, x in enumerate(xs):
+        ref = orc.process_adaptive(x, sr, n_fft=n_fft, hop=hop)
+        assert float(thr[i]) == ref["threshold"], f"stream {i}"
+        np.testing.assert_array_equal(res.stream_states(i), ref["states"])
+        a = res.stream_alpha(i)
+        assert np.array_equal(a.view(np.uint64), ref["alpha"].view(np.uint64))
+        y = res.output(i)
+        m = ref["wsum"] >= TAU
+        flag = res.scale_flags(i)[0]
+        gs = (float(np.float32(0.999) / np.float32(res.stream_peaks(i)[0]))
+              if res.stream_peaks(i)[0] > 0.999 else 1.0)
+        rs = ref["scale"] or 1.0
+        if not flag:
+            assert abs(gs / rs - 1) <= 5e-5
+            assert np.abs(y[m] - ref["y"][m]).max() <= TOL, f"stream {i}"
+        else:
+            assert np.abs(y[m] / gs - ref["y"][m] / rs).max() * min(gs, rs) <= TOL
+
+
+def test_tail_class_sweep_flags_exactly_affected():
+    """14 lengths around the golden tail case in one batch: every chunk whose
+    scale differs from the oracle's is flagged, unflagged chunks match, and the
+    one length whose reference scale is set by a tail sample is flagged."""
+    torch, E = _engine()
+    from tomatis_audio_processor_amd import conditioning
+    sr = 48000
+    lens = list(range(250784, 250876, 7))
+    xs = [synth_stream(2, n, 2, sr) for n in lens]
+    ss = E.StreamSet.from_arrays(xs, sr)
+    pipe = E.GatePipeline(ss, gate_ui=50, n_fft=2048, hop=512)
+    res = pipe.run()
+    torch.cuda.synchronize()
+    n_flag = 0
+    for i, (x, N) in enumerate(zip(xs, lens)):
+        ref = orc.process_standard(x, sr, gate_ui=50, n_fft=2048, hop=512)
+        flags = res.scale_flags(i)
+        peaks = res.stream_peaks(i)
+        y = res.output(i)
+        m = ref["wsum"][ref["pad"]:ref["pad"] + N] >= TAU
+        for c, (a, b) in enumerate(res.chunk_ranges(i)):
+            gs = float(np.float32(0.999) / np.float32(peaks[c])) if peaks[c] > 0.999 else 1.0
+            rs = ref["scales"][c] or 1.0
+            if abs(gs / rs - 1) > conditioning.ETA:
+                assert flags[c], (N, c, gs, rs)
+            if not flags[c]:
+                assert np.abs(y[a:b][m[a:b]] - ref["y"][a:b][m[a:b]]).max() <= TOL
+        n_flag += sum(flags)
+        if N == 250875:
+            assert flags[-1]
+    assert n_flag == 1

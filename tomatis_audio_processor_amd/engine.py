@@ -17,7 +17,6 @@ Reference behaviour reproduced per mode (file:line):
 from __future__ import annotations
 
 import ctypes as C
-import math
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
@@ -203,6 +202,31 @@ class Result:
         b = self.chunk_peaks[a:a + self.n_chunks[i]].cpu().numpy().astype(np.uint32)
         return b.view(np.float32)
 
+    def chunk_ranges(self, i: int):
+        """Output-index range [lo, hi) of each limiter chunk of stream ``i``."""
+        b = self.extra.get("bounds")
+        n = self.out_lens[i]
+        if not b or b[i] is None or self.n_chunks[i] <= 1:
+            return [(0, n)]
+        ob = self.extra.get("out_begin", [0] * len(self.out_lens))[i]
+        bi = b[i]
+        return [(min(n, max(0, int(bi[c]) - ob)), min(n, max(0, int(bi[c + 1]) - ob)))
+                for c in range(len(bi) - 1)]
+
+    def scale_flags(self, i: int, limit=None):
+        """Per-chunk flags: True where an ill-conditioned sample (tiny window
+        sum) may set the limiter scale, so the scale of this build
+        and of the reference may differ (conditioning.py).  ``limit``: check a
+        scale that is not applied on the device (layer-2 gain protect)."""
+        from . import conditioning
+        lim = self.extra.get("limit") if limit is None else limit
+        if lim is None:
+            return [False] * self.n_chunks[i]
+        fl = conditioning.result_flags(self, i, n_fft=self.extra["n_fft"],
+                                       norm=self.extra.get("norm", "eps"), limit=lim,
+                                       chunk_ranges=self.chunk_ranges(i))
+        return [f["flagged"] for f in fl]
+
 
 def _alloc_out(torch, lens, ch, device):
     offs, tot = [], 0
@@ -342,7 +366,9 @@ class GatePipeline:
                       chunk_peaks=self.peaks, chunk_base=[s.chunk_base for s in st],
                       n_chunks=[s.n_chunks for s in st],
                       extra=dict(Ton=self.Ton, Toff=self.Toff, T=self.T, xfade_frames=self.xf,
-                                 up_delay_samples=self.up_delay_samples, bounds=self.bounds))
+                                 up_delay_samples=self.up_delay_samples, bounds=self.bounds,
+                                 n_fft=self.n_fft, norm="eps", limit=PEAK_LIMIT,
+                                 limiter_applied=True, out_begin=[s.out_begin for s in st]))
 
 
 def _alpha_lattice(xf: int):
@@ -508,7 +534,9 @@ class AdaptivePipeline:
                       extra=dict(levels=self.levels, thresholds=self.t_out,
                                  atten_db=getattr(self, "atten", None),
                                  min_hold_frames=self.mh, xfade_frames=self.xf,
-                                 prec=getattr(self, "prec", None)))
+                                 prec=getattr(self, "prec", None), n_fft=self.n_fft,
+                                 norm="max", limit=PEAK_LIMIT, limiter_applied=True,
+                                 out_begin=[s.out_begin for s in st]))
 
 
 # ---------------------------------------------------------------------------
@@ -569,7 +597,9 @@ class StaticEqPipeline:
                       n_frames=[s.n_frames for s in st],
                       first_start=[s.first_start for s in st], hop=self.hop,
                       chunk_peaks=self.peaks, chunk_base=[s.chunk_base for s in st],
-                      n_chunks=[s.n_chunks for s in st])
+                      n_chunks=[s.n_chunks for s in st],
+                      extra=dict(n_fft=self.n_fft, norm="eps", limit=None,
+                                 limiter_applied=False, out_begin=[s.out_begin for s in st]))
 
 
 def scale_copy(src, scale: float):
@@ -664,4 +694,4 @@ def _minhold_states(levels, tlhs, hyst_db, mh, target):
 
 __all__ = ["StreamSet", "Plan", "GatePipeline", "AdaptivePipeline", "StaticEqPipeline",
            "Result", "scale_copy", "frame_r", "compute_frame_levels", "simulate_gate",
-           "find_optimal_threshold", "math"]
+           "find_optimal_threshold"]

@@ -16,7 +16,7 @@ import numpy as np
 
 # manifest record layout (int64)
 MANIFEST_FIELDS = ("stream", "rank", "frames", "c2_frames", "switches", "chunks",
-                   "limited_chunks", "peak_bits")
+                   "limited_chunks", "peak_bits", "ill_chunks")
 REC = len(MANIFEST_FIELDS)
 
 
@@ -35,15 +35,21 @@ def lpt_partition(costs: Sequence[int], n_ranks: int) -> List[List[int]]:
 
 
 def stream_records(res, stream_ids, rank: int) -> np.ndarray:
-    """Manifest rows for the streams of one ``engine.Result`` (host numpy)."""
+    """Manifest rows for the streams of one ``engine.Result`` (host numpy).
+
+    ``ill_chunks``: limiter chunks whose scale an ill-conditioned edge sample
+    may set (``Result.scale_flags``, conditioning.py), i.e. chunks whose scale
+    may differ from the reference's."""
     rows = []
     for j, sid in enumerate(stream_ids):
         st = res.stream_states(j) if res.states is not None else np.zeros(0, np.uint8)
         pk = res.stream_peaks(j) if res.chunk_peaks is not None else np.zeros(1, np.float32)
         limited = int(np.count_nonzero(pk > 0.999))
+        ill = int(sum(res.scale_flags(j))) if hasattr(res, "scale_flags") else 0
         rows.append([sid, rank, len(st), int(np.count_nonzero(st == 2)),
                      int(np.count_nonzero(st[1:] != st[:-1])) if len(st) else 0,
-                     len(pk), limited, int(np.float32(pk.max() if len(pk) else 0).view(np.uint32))])
+                     len(pk), limited, int(np.float32(pk.max() if len(pk) else 0).view(np.uint32)),
+                     ill])
     return np.asarray(rows, np.int64).reshape(-1, REC)
 
 

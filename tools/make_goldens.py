@@ -53,6 +53,10 @@ def case_input(c):
     x = synth_stream(c["seed"], c["N"], c["ch"], c["sr"])
     if c.get("in_scale") is not None:
         x = (x * np.float32(c["in_scale"])).astype(np.float32)
+    if c.get("silence"):
+        k = int(c["silence"])
+        x[:k] = 0.0
+        x[len(x) - k:] = 0.0
     return x
 
 
