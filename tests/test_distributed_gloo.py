@@ -46,7 +46,8 @@ def test_gloo_manifest_gather(ws):
     counts = {r: n for r, n, _, _ in out}
     assert sum(counts.values()) == 512 and abs(counts[0] - counts[1]) <= 2
     for _, _, shape, ids in out:
-        assert shape == (512, 8) and ids == list(range(512))
+        from tomatis_audio_processor_amd import sharding
+        assert shape == (512, sharding.REC) and ids == list(range(512))
 
 
 def _ts_worker(rank, ws, port, q):
