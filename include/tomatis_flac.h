@@ -42,7 +42,10 @@ int tomatis_flac_info(const uint8_t* data, int64_t len, int32_t* sr, int32_t* ch
                       int64_t* frames);
 
 /* Decode up to max_frames frames into pcm [max_frames][ch] (int32, stream bit
- * depth); *frames_out = frames written.  CRCs are verified. */
+ * depth); *frames_out = frames written.  CRCs are verified.  pcm == NULL with
+ * max_frames == 0 counts: *frames_out = the stream's decoded length (for
+ * streams whose STREAMINFO total is 0, "unknown").  Bytes after the last
+ * frame that do not start a verified frame (an ID3v1 tag) end the stream. */
 int tomatis_flac_decode(const uint8_t* data, int64_t len, int32_t* pcm, int64_t max_frames,
                         int64_t* frames_out);
 

@@ -249,3 +249,59 @@ def test_threaded_decode_and_encode_exact(monkeypatch):
     assert b5 == b1 and len(b1) > 5 * (1 << 20)
     y5, _, _ = audio_io.flac_decode_int(b5)
     assert np.array_equal(y1, x) and np.array_equal(y5, x)
+
+
+def _zero_total(blob: bytes) -> bytes:
+    """STREAMINFO total samples (36 bits at byte 8+13.5) set to 0 = unknown."""
+    b = bytearray(blob)
+    b[8 + 13] &= 0xF0
+    b[8 + 14:8 + 18] = b"\0\0\0\0"
+    return bytes(b)
+
+
+def test_unknown_total_decodes_exactly(tmp_path):
+    """A STREAMINFO total of 0 ("unknown", legal; written by encoders that
+    stream to a pipe) decodes to the exact samples, through audio_io too."""
+    rng = np.random.default_rng(5)
+    x = rng.integers(-(1 << 23), 1 << 23, size=(50001, 2)).astype(np.int32)
+    blob = _zero_total(audio_io.flac_encode_int(x, 48000, 24))
+    assert audio_io.flac_info_bytes(blob)[3] == 0
+    y, sr, bps = audio_io.flac_decode_int(blob)
+    assert np.array_equal(y, x)
+    p = tmp_path / "u.flac"
+    p.write_bytes(blob)
+    assert audio_io.info(str(p)) == (48000, 2, 50001)
+    z, _ = audio_io.read(str(p))
+    assert z.shape == (50001, 2)
+
+
+@pytest.mark.parametrize("unknown_total", [False, True])
+def test_id3_tags_are_skipped(tmp_path, unknown_total):
+    """A leading ID3v2 tag and a trailing 128-byte ID3v1 'TAG' block (both
+    accepted by libsndfile) do not stop the decode or change the samples."""
+    rng = np.random.default_rng(6)
+    x = rng.integers(-30000, 30000, size=(30000, 1)).astype(np.int32)
+    blob = audio_io.flac_encode_int(x, 44100, 16)
+    if unknown_total:
+        blob = _zero_total(blob)
+    body = b"\x00" * 300
+    sz = len(body)
+    id3 = b"ID3\x04\x00\x00" + bytes([(sz >> 21) & 0x7F, (sz >> 14) & 0x7F, (sz >> 7) & 0x7F,
+                                      sz & 0x7F]) + body
+    tag = b"TAG" + b"title".ljust(30, b"\0") + bytes(95)
+    p = tmp_path / "t.flac"
+    p.write_bytes(id3 + blob + tag)
+    assert audio_io.info(str(p)) == (44100, 1, 30000)
+    z, sr = audio_io.read(str(p))
+    assert sr == 44100 and np.array_equal(np.rint(z * 32768.0).astype(np.int32), x)
+    y, _, _ = audio_io.flac_decode_int(blob + tag)
+    assert np.array_equal(y, x)
+
+
+def test_corrupt_last_frame_of_unknown_total_is_an_error():
+    rng = np.random.default_rng(7)
+    x = rng.integers(-1000, 1000, size=(9000, 2)).astype(np.int32)
+    b = bytearray(_zero_total(audio_io.flac_encode_int(x, 44100, 16)))
+    b[len(b) - 1] ^= 0x10          # frame CRC-16 of a frame that starts with a sync code
+    with pytest.raises(audio_io.AudioFormatError):
+        audio_io.flac_decode_int(bytes(b))

@@ -170,3 +170,12 @@ def test_level_stats_bit_identical_to_numpy():
         got = np.array(dsp.level_stats(v))
         ref = np.array([np.percentile(v, 5), np.percentile(v, 95), np.median(v)])
         assert np.array_equal(got.view(np.uint64), ref.view(np.uint64)), (n, got, ref)
+
+
+def test_batch_output_names_unique():
+    """Inputs with the same file name in different directories get distinct
+    outputs (no silent overwrite across or within ranks)."""
+    from tomatis_audio_processor_amd.batch import output_names
+    names = output_names(["a/x.wav", "b/x.wav", "c/y.flac", "x.flac"], "wav")
+    assert names == ["x_0_tomatis.wav", "x_1_tomatis.wav", "y_tomatis.wav", "x_3_tomatis.wav"]
+    assert len(set(names)) == len(names)

@@ -95,9 +95,23 @@ def flac_info_bytes(data: bytes):
     return sr.value, ch.value, bps.value, n.value
 
 
+def flac_count_frames(data: bytes) -> int:
+    """Decoded length of a FLAC stream (decodes without storing samples)."""
+    got = C.c_int64()
+    rc = _flac().tomatis_flac_decode(data, len(data), None, 0, C.byref(got))
+    if rc:
+        raise AudioFormatError(f"FLAC decode failed: {_FLAC_ERR.get(rc, rc)}")
+    return got.value
+
+
 def flac_decode_int(data: bytes):
-    """(int32 PCM [frames, ch], sr, bps) of an in-memory FLAC stream."""
+    """(int32 PCM [frames, ch], sr, bps) of an in-memory FLAC stream.
+
+    A STREAMINFO total of 0 means "unknown" in the FLAC format (encoders
+    writing to a pipe leave it so); the length is then counted first."""
     sr, ch, bps, n = flac_info_bytes(data)
+    if n == 0:
+        n = flac_count_frames(data)
     pcm = np.empty((n, ch), np.int32)
     got = C.c_int64()
     rc = _flac().tomatis_flac_decode(data, len(data), pcm.ctypes.data, n, C.byref(got))
@@ -106,10 +120,25 @@ def flac_decode_int(data: bytes):
     return pcm[:got.value], sr, bps
 
 
-def _read_flac(path: str):
+def id3v2_size(head: bytes) -> int:
+    """Bytes taken by a leading ID3v2 tag (0 if none): 10-byte header, syncsafe
+    size, plus a 10-byte footer when flagged.  libsndfile skips it too."""
+    if len(head) < 10 or head[:3] != b"ID3":
+        return 0
+    sz = 0
+    for b in head[6:10]:
+        sz = (sz << 7) | (b & 0x7F)
+    return 10 + sz + (10 if head[5] & 0x10 else 0)
+
+
+def _flac_bytes(path: str) -> bytes:
     with open(path, "rb") as f:
         data = f.read()
-    pcm, sr, bps = flac_decode_int(data)
+    return data[id3v2_size(data[:10]):]
+
+
+def _read_flac(path: str):
+    pcm, sr, bps = flac_decode_int(_flac_bytes(path))
     # libsndfile's int -> float normalisation: v / 2^(bps-1)
     x = (pcm.astype(np.float64) / float(1 << (bps - 1))).astype(np.float32)
     return np.ascontiguousarray(x), sr
@@ -135,6 +164,9 @@ def _sniff(path: str):
     whatever name ``-o`` gives, src/process_tomatis_xfade.py:115)."""
     try:
         with open(path, "rb") as f:
+            head = f.read(10)
+            k = id3v2_size(head)
+            f.seek(k)
             m = f.read(4)
     except OSError:
         return None
@@ -148,8 +180,12 @@ def info(path: str):
         return i.samplerate, i.channels, i.frames
     if _sniff(path) == "flac":
         with open(path, "rb") as f:
+            k = id3v2_size(f.read(10))
+            f.seek(k)
             head = f.read(42)
         sr, ch, _, n = flac_info_bytes(head)
+        if n == 0:   # total unknown in STREAMINFO: count the frames
+            n = flac_count_frames(_flac_bytes(path))
         return sr, ch, n
     fmt, ch, sr, bits, data_off, data_len = _parse_wav_header(path)
     return sr, ch, data_len // (ch * (bits // 8))

@@ -37,10 +37,23 @@ def _dist():
     return rank, ws
 
 
+def output_names(inputs, ext):
+    """``<stem>_tomatis.<ext>`` per input; inputs whose stems collide (same file
+    name in different directories) get their input index appended, so no rank
+    overwrites another stream's output.  Every rank computes the same names."""
+    stems = [os.path.splitext(os.path.basename(p))[0] for p in inputs]
+    count = defaultdict(int)
+    for s in stems:
+        count[s] += 1
+    return [f"{s}_tomatis.{ext}" if count[s] == 1 else f"{s}_{i}_tomatis.{ext}"
+            for i, s in enumerate(stems)]
+
+
 def run(args):
     import torch
     from . import engine
     rank, ws = _dist()
+    names = output_names(args.input, args.out_ext)
     infos = [audio_io.info(p) for p in args.input]
     costs = [fr * ch for (sr, ch, fr) in infos]
     mine = sharding.lpt_partition(costs, ws)[rank]
@@ -64,8 +77,7 @@ def run(args):
         res = pipe.run()
         torch.cuda.synchronize()
         for j, i in enumerate(ids):
-            base = os.path.splitext(os.path.basename(args.input[i]))[0]
-            out = os.path.join(args.out_dir, f"{base}_tomatis.{args.out_ext}")
+            out = os.path.join(args.out_dir, names[i])
             if args.out_ext == "wav":
                 audio_io.write(out, res.output(j), sr, "WAV", "PCM_24")
             else:
@@ -75,8 +87,8 @@ def run(args):
     dev = "cuda" if (ws > 1 and torch.cuda.is_available()) else None
     allrec = sharding.gather_manifest(rec, device=dev)
     if rank == 0:
-        man = [dict(zip(sharding.MANIFEST_FIELDS, map(int, r)), path=args.input[int(r[0])])
-               for r in allrec]
+        man = [dict(zip(sharding.MANIFEST_FIELDS, map(int, r)), path=args.input[int(r[0])],
+                    out=names[int(r[0])]) for r in allrec]
         with open(os.path.join(args.out_dir, "manifest.json"), "w") as f:
             json.dump({"world_size": ws, "streams": man}, f, indent=1)
         print(f"[DONE] {len(man)} streams on {ws} GPU(s) -> {args.out_dir}/manifest.json")

@@ -599,11 +599,31 @@ int decode_frame(const uint8_t* d, size_t len, size_t p, int ch0, int bps0, int6
   return TOMATIS_FLAC_OK;
 }
 
+// true when no frame that verifies (header CRC-8 and frame CRC-16) starts in
+// [p, len): the bytes there are not audio (an ID3v1 'TAG' block, padding)
+bool no_frame_after(const uint8_t* d, size_t len, size_t p, int ch0, int bps0, int64_t nominal,
+                    std::vector<int64_t>* sub) {
+  for (; p + 1 < len; ++p) {
+    if (!(d[p] == 0xFF && (d[p + 1] & 0xFE) == 0xF8)) continue;
+    size_t used;
+    int64_t e;
+    if (decode_frame(d, len, p, ch0, bps0, nominal, nullptr, 0, sub, &used, &e) ==
+        TOMATIS_FLAC_OK)
+      return false;
+  }
+  return true;
+}
+
 // Frames whose first byte lies in [lo, hi): the first one is found by sync
 // search (0xFFF8/0xFFF9 with a valid header and frame CRC), the rest follow.
+// Bytes that fail to decode end the stream (no error) when the decoded end
+// has reached STREAMINFO's total, or, for a stream of unknown total, when they
+// do not start with a frame sync code and no verified frame follows them:
+// trailing non-audio bytes (an ID3v1 tag), which libsndfile accepts.  A frame
+// that starts with a sync code and fails its CRC stays an error.
 void decode_range(const uint8_t* d, size_t len, size_t lo, size_t hi, bool exact_start, int ch0,
-                  int bps0, int64_t nominal, int32_t* pcm, int64_t max_frames, int* rc,
-                  int64_t* end) {
+                  int bps0, int64_t nominal, int64_t total, int32_t* pcm, int64_t max_frames,
+                  int* rc, int64_t* end) {
   std::vector<int64_t> sub[8];
   size_t p = lo;
   *rc = TOMATIS_FLAC_OK;
@@ -628,6 +648,10 @@ void decode_range(const uint8_t* d, size_t len, size_t lo, size_t hi, bool exact
     int64_t e;
     const int r = decode_frame(d, len, p, ch0, bps0, nominal, pcm, max_frames, sub, &used, &e);
     if (r) {
+      const bool sync = d[p] == 0xFF && (d[p + 1] & 0xFE) == 0xF8;
+      if ((total > 0 && *end >= total) ||
+          (total == 0 && !sync && no_frame_after(d, len, p + 1, ch0, bps0, nominal, sub)))
+        return;
       *rc = r;
       return;
     }
@@ -756,11 +780,11 @@ int tomatis_flac_decode(const uint8_t* d, int64_t len, int32_t* pcm, int64_t max
   for (int t = 0; t < nt; ++t) {
     const size_t lo = p + body * t / nt, hi = p + body * (t + 1) / nt;
     if (t == nt - 1)
-      decode_range(d, (size_t)len, lo, (size_t)len, t == 0, ch0, bps0, nominal, pcm, max_frames,
-                   &rcs[t], &ends[t]);
+      decode_range(d, (size_t)len, lo, (size_t)len, t == 0, ch0, bps0, nominal, total, pcm,
+                   max_frames, &rcs[t], &ends[t]);
     else
-      th.emplace_back(decode_range, d, (size_t)len, lo, hi, t == 0, ch0, bps0, nominal, pcm,
-                      max_frames, &rcs[t], &ends[t]);
+      th.emplace_back(decode_range, d, (size_t)len, lo, hi, t == 0, ch0, bps0, nominal, total,
+                      pcm, max_frames, &rcs[t], &ends[t]);
   }
   for (auto& x : th) x.join();
   int64_t done = 0;
@@ -769,7 +793,8 @@ int tomatis_flac_decode(const uint8_t* d, int64_t len, int32_t* pcm, int64_t max
     done = std::max(done, ends[t]);
   }
   if (total) done = std::min(done, total);
-  if (frames_out) *frames_out = std::min(done, max_frames);
+  // counting mode (pcm == NULL, max_frames == 0): the decoded length
+  if (frames_out) *frames_out = pcm ? std::min(done, max_frames) : done;
   return TOMATIS_FLAC_OK;
 }
 
