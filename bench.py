@@ -103,8 +103,47 @@ def dist_init():
     return rank, ws, local
 
 
-def cpu_baseline(sample_s: int, sr: int, n_fft: int, hop: int, ch: int, x_host=None):
-    """Time the oracle ('port' of the reference loop) on one host core."""
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def _host_cores() -> int:
+    """Cores this process may use: the affinity mask, capped at the GPU box's
+    per-GPU CPU share (16)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def _pool_task(args):
+    """One stream through the oracle in a worker process (1 BLAS/OMP thread)."""
+    seed, n, ch, sr, n_fft, hop = args
+    from oracle import tomatis_oracle as orc
+    from tomatis_audio_processor_amd.synth import synth_stream
+    x = synth_stream(seed, n, ch, sr)
+    t0 = time.perf_counter()
+    orc.process_standard(x, sr, gate_ui=50, n_fft=n_fft, hop=hop)
+    return time.perf_counter() - t0
+
+
+def cpu_baseline(sample_s: int, sr: int, n_fft: int, hop: int, ch: int, x_host=None,
+                 pool_s: int = 300):
+    """The oracle (a 'port' of the reference loop) on the host:
+    (1) one core over the first ``sample_s`` s of the bench stream; (2) file-
+    parallel over P = host cores, one process per core, P streams of ``pool_s``
+    s each (seeds 1000..), aggregate = all channel-samples / the slowest
+    worker's busy time."""
+    import multiprocessing as mp
     from oracle import tomatis_oracle as orc
     from tomatis_audio_processor_amd.synth import synth_stream
     n = sample_s * sr
@@ -112,11 +151,25 @@ def cpu_baseline(sample_s: int, sr: int, n_fft: int, hop: int, ch: int, x_host=N
     t0 = time.perf_counter()
     orc.process_standard(x, sr, gate_ui=50, n_fft=n_fft, hop=hop)
     dt = time.perf_counter() - t0
-    return {"value": round(n * ch / dt / 1e6, 3), "unit": "Msamples/s", "cores": 1,
-            "kind": "port",
-            "sample": f"first {sample_s} s of stream seed 1000 ({n} x {ch} ch, {sr} Hz), "
-                      f"oracle/tomatis_oracle.process_standard (numpy {np.__version__}), "
-                      f"1 thread, {dt:.2f} s"}
+    one = round(n * ch / dt / 1e6, 3)
+    P = _host_cores()
+    pool_val, pool_note = None, ""
+    if P > 1 and pool_s > 0:
+        for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS"):
+            os.environ[k] = "1"
+        npool = pool_s * sr
+        tasks = [(1000 + i, npool, ch, sr, n_fft, hop) for i in range(P)]
+        with mp.get_context("spawn").Pool(P) as pool:
+            dts = pool.map(_pool_task, tasks, chunksize=1)
+        pool_val = round(P * npool * ch / max(dts) / 1e6, 3)
+        pool_note = (f"; {P} processes x one {pool_s} s stream each (seeds 1000..{999 + P}), "
+                     f"slowest worker {max(dts):.2f} s")
+    return {"value": pool_val if pool_val is not None else one, "unit": "Msamples/s",
+            "cores": P if pool_val is not None else 1, "kind": "port",
+            "single_core": one, "cpu_model": _cpu_model(), "numpy": np.__version__,
+            "sample": f"oracle/tomatis_oracle.process_standard (numpy {np.__version__}) on "
+                      f"{_cpu_model()}: 1 core over the first {sample_s} s of stream seed 1000 "
+                      f"({n} x {ch} ch, {sr} Hz) in {dt:.2f} s = {one} Msamples/s" + pool_note}
 
 
 def load_traffic(workload: str):
@@ -131,6 +184,21 @@ def load_traffic(workload: str):
         return None
 
 
+def relaunch(n: int) -> int:
+    """``--gpus N`` without a launcher: start torch.distributed.run with N
+    ranks as a CHILD process (nothing here has touched the GPU) and relay its
+    output and exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -138,8 +206,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--cpu-sample-s", type=int, default=3600,
-                    help="seconds of audio for the CPU baseline (0 disables)")
+                    help="seconds of audio for the 1-core CPU baseline (0 disables the baseline)")
+    ap.add_argument("--cpu-pool-s", type=int, default=300,
+                    help="seconds of audio per worker for the all-cores CPU baseline")
     a = ap.parse_args()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        raise SystemExit(relaunch(a.gpus))
+    ws_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws_env != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={ws_env}: launch one rank per GPU")
 
     import torch
     import torch.distributed as dist
@@ -225,7 +300,7 @@ def main():
         cpu = None
         if a.cpu_sample_s > 0 and mode == "standard" and not strong:
             xs = ss.x[:a.cpu_sample_s * sr * ch].cpu().numpy().reshape(-1, ch)
-            cpu = cpu_baseline(a.cpu_sample_s, sr, n_fft, hop, ch, x_host=xs)
+            cpu = cpu_baseline(a.cpu_sample_s, sr, n_fft, hop, ch, x_host=xs, pool_s=a.cpu_pool_s)
         out = {
             "metric": "Msamples/s (44.1 kHz stereo) end-to-end STFT-gate-OLA; % HBM roofline",
             "value": round(value, 1), "unit": "Msamples/s", "n_gpus": ws, "steps": a.steps,
