@@ -179,3 +179,21 @@ def test_batch_output_names_unique():
     names = output_names(["a/x.wav", "b/x.wav", "c/y.flac", "x.flac"], "wav")
     assert names == ["x_0_tomatis.wav", "x_1_tomatis.wav", "y_tomatis.wav", "x_3_tomatis.wav"]
     assert len(set(names)) == len(names)
+
+
+def test_level_nonmonotone_steps_are_isolated():
+    """Exhaustive over every finite float32 r >= 2^-20 (r >= 1e-6 always): the
+    reference's level 20*log10(f32(r)+EPS) steps down at isolated points, each
+    far more than gate_bits' +-8192-ulp window from the next, so no crossing
+    window can hold more than one exception (the 4-entry table never overflows)."""
+    lo = int(np.float32(2.0 ** -20).view(np.uint32))
+    hi = 0x7F7FFFFF
+    bad = []
+    step = 1 << 23
+    with np.errstate(over="ignore"):
+        for a in range(lo, hi, step):
+            b = np.arange(a, min(a + step + 1, hi + 1), dtype=np.uint32)
+            lv = (20.0 * np.log10(b.view(np.float32) + 1e-12)).astype(np.float64)
+            bad.extend((b[np.nonzero(lv[1:] < lv[:-1])[0]]).tolist())
+    assert 0 < len(bad) < 64
+    assert np.min(np.diff(np.asarray(bad, np.int64))) > 4 * 8192

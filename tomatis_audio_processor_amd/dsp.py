@@ -150,6 +150,11 @@ def gate_bits(Ton: float, Toff: float):
     off_exc = [int(b) for b in w2[(w2 <= off_bits) & ~pw2]]
     if off_bits < 0:  # never true: b <= 0 with b == 0 flipped off by an exception
         off_bits, off_exc = 0, [0]
+    # Unreachable for any finite threshold: every r is >= 1e-6 (the +EPS under the
+    # square root), and over all finite float32 r >= 2^-20 numpy's level has 35
+    # non-monotone steps, each >= 2^23 ulps from the next, so a +-8192-ulp
+    # window holds at most one (tests/test_host_logic.py scans all 1.3e9
+    # patterns).  Kept as a guard for a numpy whose log10 behaves otherwise.
     if len(on_exc) > 4 or len(off_exc) > 4:
         raise RuntimeError("gate threshold crossing too irregular for the exception table")
     return on_bits, on_exc, off_bits, off_exc
