@@ -38,6 +38,11 @@
  *   src/validate_layer1.py:261-389               tomatis_an_frame_r, tomatis_an_select,
  *       (compute_conditional_spectrum)            tomatis_an_spectra(RATIO),
  *                                                 tomatis_an_frame_median
+ *   src/calibrate_to_baseline_v2.py:192-198      tomatis_an_frame_r (POWER_MONO levels),
+ *       (orig/base levels, stft_band_tilt :17-31)  tomatis_an_band_energy
+ *   src/calibrate_to_baseline_v2.py:84-109,      tomatis_cal_gate_grid
+ *       231-265 (simulate_state x the gain /
+ *       up-delay / hysteresis / T search grid)
  *
  * Conventions: every call is asynchronous on the given hipStream_t and returns
  * an int status (0 = ok, <0 = error, see TOMATIS_E_*); no exceptions cross the
@@ -273,6 +278,38 @@ int64_t tomatis_an_median_work_words(int32_t n_bins);
 int tomatis_an_frame_median(const float* spec, int32_t n_frames, int32_t n_bins,
                             const uint8_t* mask, int32_t n_sel, uint32_t* work, float* out,
                             void* hip_stream);
+
+/* ---------------------------------------------------------------------------
+ * Gate calibration (src/calibrate_to_baseline_v2.py).
+ * ------------------------------------------------------------------------- */
+
+/* Per-frame band energies of rfft(win * power_mono(x)) for stereo x
+ * (stft_band_tilt, calibrate_to_baseline_v2.py:17-31): out[f][0] = sum of the
+ * float32 power re^2+im^2 over bins [lo0, lo1), out[f][1] over [hi0, hi1).
+ * Frames as tomatis_an_spectra; n_fft a power of two in [256, 8192]. */
+int tomatis_an_band_energy(const float* x, int64_t n, int32_t n_fft, int32_t hop,
+                           int32_t lo0, int32_t lo1, int32_t hi0, int32_t hi1,
+                           const float* win, float* out, void* hip_stream);
+
+/* One candidate of the gate-calibration grid: thresholds already rounded to
+ * float32 (numpy compares an np.float32 level with a Python float in float32),
+ * up-delay in samples (int(round(sr * up_ms / 1000))), level row index. */
+typedef struct TomatisGateCand {
+    int32_t level_row;    /* row of `levels` (one per searched gain)          */
+    float t_on, t_off;    /* float32(T + hyst/2), float32(T - hyst/2)         */
+    int32_t pad_;
+    int64_t up_delay;     /* samples                                          */
+} TomatisGateCand;
+
+/* For every candidate c: the standard gate automaton of simulate_state
+ * (calibrate_to_baseline_v2.py:84-109) over frames i < n_fit with levels
+ * levels[c.level_row * n_fit + i] (float32) and frame starts starts[i];
+ * out[2c] = #frames whose state != target[i] (1/2; 0 if target is NULL),
+ * out[2c+1] = #switches; states (optional, [n_cand][n_fit] u8) = the state
+ * sequence itself.  All buffers device-resident; cands: n_cand records. */
+int tomatis_cal_gate_grid(const float* levels, int32_t n_fit, const int64_t* starts,
+                          const int32_t* target, const TomatisGateCand* cands, int32_t n_cand,
+                          int32_t* out, uint8_t* states, void* hip_stream);
 
 #ifdef __cplusplus
 }

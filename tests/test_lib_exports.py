@@ -44,8 +44,9 @@ def test_struct_layout_matches_header():
 #include <stdio.h>
 #include <stddef.h>
 #include "tomatis_hip.h"
-int main(){printf("%zu %zu %zu %zu %zu\n", sizeof(TomatisStream), offsetof(TomatisStream,t_on),
- offsetof(TomatisStream,frame_base), sizeof(TomatisPlanDesc), offsetof(TomatisStream,on_exc));return 0;}
+int main(){printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(TomatisStream), offsetof(TomatisStream,t_on),
+ offsetof(TomatisStream,frame_base), sizeof(TomatisPlanDesc), offsetof(TomatisStream,on_exc),
+ sizeof(TomatisGateCand), offsetof(TomatisGateCand,up_delay));return 0;}
 '''
     with tempfile.TemporaryDirectory() as d:
         src = os.path.join(d, "s.c")
@@ -54,8 +55,12 @@ int main(){printf("%zu %zu %zu %zu %zu\n", sizeof(TomatisStream), offsetof(Tomat
         subprocess.run(["gcc", "-I" + os.path.join(ROOT, "include"), src, "-o", exe], check=True)
         out = subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()
     S = _lib.TomatisStream
+    G = _lib.TomatisGateCand
     got = [ctypes.sizeof(S), S.t_on.offset, S.frame_base.offset,
-           ctypes.sizeof(_lib.TomatisPlanDesc), S.on_exc.offset]
+           ctypes.sizeof(_lib.TomatisPlanDesc), S.on_exc.offset, ctypes.sizeof(G),
+           G.up_delay.offset]
+    import numpy as np
+    assert np.dtype(_lib.GATE_CAND_DTYPE).itemsize == ctypes.sizeof(G)
     assert [int(v) for v in out] == got
 
 

@@ -43,6 +43,16 @@ class TomatisStream(C.Structure):
     ]
 
 
+class TomatisGateCand(C.Structure):
+    """Mirror of ``TomatisGateCand`` in include/tomatis_hip.h (24 bytes)."""
+    _fields_ = [("level_row", C.c_int32), ("t_on", C.c_float), ("t_off", C.c_float),
+                ("pad_", C.c_int32), ("up_delay", C.c_int64)]
+
+
+GATE_CAND_DTYPE = [("level_row", "<i4"), ("t_on", "<f4"), ("t_off", "<f4"), ("pad_", "<i4"),
+                   ("up_delay", "<i8")]
+
+
 class TomatisPlanDesc(C.Structure):
     _fields_ = [
         ("n_fft", C.c_int32), ("hop", C.c_int32), ("ch", C.c_int32),
@@ -89,6 +99,10 @@ _SIGS = {
     "tomatis_an_frame_mean": (C.c_int, [_P, C.c_int32, C.c_int32, _P, _P]),
     "tomatis_an_median_work_words": (C.c_int64, [C.c_int32]),
     "tomatis_an_frame_median": (C.c_int, [_P, C.c_int32, C.c_int32, _P, C.c_int32, _P, _P, _P]),
+    # gate calibration
+    "tomatis_an_band_energy": (C.c_int, [_P, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
+                                         C.c_int32, C.c_int32, C.c_int32, _P, _P, _P]),
+    "tomatis_cal_gate_grid": (C.c_int, [_P, C.c_int32, _P, _P, _P, C.c_int32, _P, _P, _P]),
 }
 EXPORTS = tuple(_SIGS)
 

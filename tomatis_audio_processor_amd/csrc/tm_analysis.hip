@@ -291,6 +291,7 @@ struct SpecArgs {
   float* out;
   int n_fft, logn, hop, n_frames, n_bins;
   float sc;
+  int band[4];  // TOMATIS_AN_BAND: bins [band0, band1) and [band2, band3)
 };
 
 template <int SIG>  // TOMATIS_AN_SIG_RAW (ch 1) / TOMATIS_AN_SIG_POWER_MONO (ch 2)
@@ -334,6 +335,101 @@ __global__ __launch_bounds__(kT) void k_an_spec_pair(SpecArgs A) {
       }
     }
   }
+}
+
+// BAND (stft_band_tilt, calibrate_to_baseline_v2.py:17-31): per frame of the
+// pair the float32 power re^2 + im^2 of rfft(win * power_mono) summed over two
+// bin ranges; workgroup per frame pair as k_an_spec_pair, block reduction.
+template <int N>
+__global__ __launch_bounds__(kT) void k_an_band_pair(SpecArgs A) {
+  __shared__ float2 buf[N];
+  __shared__ float red[kT / 64][4];
+  const int f0 = blockIdx.x * 2, f1 = f0 + 1;
+  const bool has1 = f1 < A.n_frames;
+  const int64_t p0 = (int64_t)f0 * A.hop, p1 = (int64_t)f1 * A.hop;
+  for (int i = threadIdx.x; i < N; i += kT) {
+    const float w = A.win[i];
+    const float a = power_mono(A.x, p0 + i, A.sc) * w;
+    const float b = has1 ? power_mono(A.x, p1 + i, A.sc) * w : 0.f;
+    buf[i] = make_float2(a, b);
+  }
+  __syncthreads();
+  lds_fft<N>(buf, A.tw);
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};  // (frame a, band lo), (a, hi), (b, lo), (b, hi)
+  for (int k = threadIdx.x; k < A.n_bins; k += kT) {
+    const bool lo = k >= A.band[0] && k < A.band[1], hi = k >= A.band[2] && k < A.band[3];
+    if (!lo && !hi) continue;
+    const float2 zk = buf[k], zm = buf[(N - k) & (N - 1)];
+    const float2 fa = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
+    const float2 fb = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
+    const float pa = fa.x * fa.x + fa.y * fa.y, pb = fb.x * fb.x + fb.y * fb.y;
+    acc[hi ? 1 : 0] += pa;
+    acc[hi ? 3 : 2] += pb;
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float v = acc[j];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if (lane == 0) red[w][j] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    float v = 0.f;
+    for (int i = 0; i < kT / 64; ++i) v += red[i][threadIdx.x];
+    const int j = threadIdx.x;
+    if (j < 2) A.out[(int64_t)f0 * 2 + j] = v;
+    else if (has1) A.out[(int64_t)f1 * 2 + (j - 2)] = v;
+  }
+}
+
+// Gate-calibration grid (calibrate_to_baseline_v2.py:84-109 simulate_state,
+// :241-265 the search): one lane per candidate runs the standard automaton
+// (hysteresis + up-delay on frame starts) over the fitted frames and counts
+// mismatches against the target states and state switches.  Levels are
+// float32 and compared with the float32 thresholds exactly as numpy compares
+// an np.float32 level with a Python float (NEP 50: in float32).
+__global__ __launch_bounds__(256) void k_cal_gate_grid(const float* __restrict__ levels,
+                                                       int n_fit,
+                                                       const int64_t* __restrict__ starts,
+                                                       const int32_t* __restrict__ target,
+                                                       const TomatisGateCand* __restrict__ cands,
+                                                       int n_cand, int32_t* __restrict__ out,
+                                                       uint8_t* __restrict__ states) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n_cand) return;  // no barriers below
+  const TomatisGateCand C = cands[c];
+  const float* lv = levels + (int64_t)C.level_row * n_fit;
+  int state = 1, prev = 1, mism = 0, sw = 0;
+  bool pend = false;
+  int64_t pending = 0;
+  for (int i = 0; i < n_fit; ++i) {
+    const float l = lv[i];
+    const int64_t st = starts[i];
+    if (state == 1) {
+      if (l >= C.t_on) {
+        if (!pend) {
+          pend = true;
+          pending = st + C.up_delay;
+        }
+      } else {
+        pend = false;
+      }
+      if (pend && st >= pending) {
+        state = 2;
+        pend = false;
+      }
+    } else if (l <= C.t_off) {
+      state = 1;
+      pend = false;
+    }
+    if (states) states[(int64_t)c * n_fit + i] = (uint8_t)state;
+    if (target) mism += state != target[i];
+    sw += (i > 0) & (state != prev);
+    prev = state;
+  }
+  out[2 * c] = mism;
+  out[2 * c + 1] = sw;
 }
 
 // RATIO: workgroup per frame; per channel one FFT of x_c + i y_c
@@ -617,6 +713,42 @@ int tomatis_an_spectra(const float* x, const float* y, int64_t n, int32_t ch, in
   AN_PAIR(TOMATIS_AN_LOGPOW, TOMATIS_AN_SIG_POWER_MONO)
 #undef AN_PAIR
 #undef AN_PAIR_N
+  return an_launch();
+}
+
+int tomatis_an_band_energy(const float* x, int64_t n, int32_t n_fft, int32_t hop,
+                           int32_t lo0, int32_t lo1, int32_t hi0, int32_t hi1,
+                           const float* win, float* out, void* hs) {
+  const int logn = ilog2_pow2(n_fft);
+  if (!x || !win || !out || hop < 1) return TOMATIS_E_ARG;
+  if (logn < 8 || n_fft > kMaxN) return TOMATIS_E_UNSUPPORTED;
+  const int nb = n_fft / 2 + 1;
+  if (lo0 < 0 || lo1 < lo0 || lo1 > nb || hi0 < 0 || hi1 < hi0 || hi1 > nb) return TOMATIS_E_ARG;
+  if (lo1 > hi0 && hi1 > lo0) return TOMATIS_E_ARG;  // bands must not overlap
+  if (n < n_fft) return TOMATIS_OK;
+  const int64_t F = 1 + (n - n_fft) / hop;
+  if (F > INT32_MAX) return TOMATIS_E_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)hs;
+  SpecArgs A{x, nullptr, win, nullptr, out, n_fft, logn, hop, (int)F, nb, 1.0f,
+             {lo0, lo1, hi0, hi1}};
+  int rc = twiddles(n_fft, s, &A.tw);
+  if (rc != TOMATIS_OK) return rc;
+  const dim3 g((unsigned)((F + 1) / 2));
+#define AN_BAND(NN) \
+  if (n_fft == NN) hipLaunchKernelGGL((k_an_band_pair<NN>), g, dim3(kT), 0, s, A);
+  AN_BAND(256) AN_BAND(512) AN_BAND(1024) AN_BAND(2048) AN_BAND(4096) AN_BAND(8192)
+#undef AN_BAND
+  return an_launch();
+}
+
+int tomatis_cal_gate_grid(const float* levels, int32_t n_fit, const int64_t* starts,
+                          const int32_t* target, const TomatisGateCand* cands, int32_t n_cand,
+                          int32_t* out, uint8_t* states, void* hs) {
+  if (n_fit < 0 || n_cand < 0 || (n_cand && (!cands || !out)) || (n_fit && (!levels || !starts)))
+    return TOMATIS_E_ARG;
+  if (n_cand == 0) return TOMATIS_OK;
+  hipLaunchKernelGGL(k_cal_gate_grid, dim3((n_cand + 255) / 256), dim3(256), 0,
+                     (hipStream_t)hs, levels, n_fit, starts, target, cands, n_cand, out, states);
   return an_launch();
 }
 
