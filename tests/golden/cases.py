@@ -40,6 +40,11 @@ CASES = [
     # found by tools/find_tail_cases.py (1 of 440 lengths near 250 k)
     dict(name="std_48k_st_tail_ill", mode="standard", sr=S48, ch=2, N=250875,
          seed=2, params=dict(gate_ui=50, n_fft=2048, hop=512)),
+    # any-size LDS path (n_fft other than 2048/4096; SURVEY §8 b "any --n_fft")
+    dict(name="std_48k_st_1024_256", mode="standard", sr=S48, ch=2, N=96000 + 1024 + 77,
+         seed=9, params=dict(gate_ui=50, n_fft=1024, hop=256)),
+    dict(name="std_48k_st_8192_2048", mode="standard", sr=S48, ch=2, N=288000 + 8192 + 555,
+         seed=10, params=dict(gate_ui=50, n_fft=8192, hop=2048)),
     # --- xfade (src/process_tomatis_xfade.py) ------------------------------
     dict(name="xfade_48k_st_2048_512_500ms", mode="xfade", sr=S48, ch=2,
          N=288000 + 5000, seed=11,
@@ -59,6 +64,11 @@ CASES = [
          N=44100 * 6 + 123, seed=22, in_scale=0.01, params=dict(n_fft=2048, hop=512)),
     dict(name="adapt_48k_mono_4096_2048", mode="adaptive", sr=S48, ch=1,
          N=48000 * 7, seed=23, params=dict()),
+    # the adaptive processor takes any channel count (no guard, adaptive.py:179-183)
+    dict(name="adapt_48k_4ch_2048_512", mode="adaptive", sr=S48, ch=4, N=48000 * 5 + 321,
+         seed=24, params=dict(n_fft=2048, hop=512)),
+    dict(name="adapt_44k_st_512_128", mode="adaptive", sr=S44, ch=2, N=44100 * 4 + 99,
+         seed=25, params=dict(n_fft=512, hop=128)),
     # --- layer 2 (src/layer2_apply_eq.py) -----------------------------------
     dict(name="l2_48k_st_pad_gp", mode="layer2", sr=S48, ch=2, N=150000 + 17,
          seed=31, params=dict(n_fft=2048, hop=512)),

@@ -968,6 +968,8 @@ struct tomatis_plan_s {
   int32_t total_chunks = 0;
   int P = 0, NR = 32, SH = 0, rmax = 1;
   bool generic = false;
+  bool lds = false;        // any-size path (k_stft_lds + k_ola_gather_lds)
+  float2* twL = nullptr;   // lds path: exp(-2 pi i t / N)
   std::vector<TomatisStream> hs;
   int lvl_nf = 0;
   // device
@@ -1074,7 +1076,7 @@ int tomatis_plan_destroy(tomatis_plan_t p) {
                   p->pos_base, p->chunks, p->mh_tf, p->mh_cnt, p->mh_off, p->gperm,
                   p->grp_base, p->leaf_base, p->leaves, p->gsum, p->gcarry, p->gcarry_in,
                   p->aq, p->afin, p->acin,
-                  p->chunk_need, p->chunk_done, p->chunk_rng, p->err};
+                  p->chunk_need, p->chunk_done, p->chunk_rng, p->err, p->twL};
   for (void* q : ptrs) dfree(q);
   delete p;
   return TOMATIS_OK;
@@ -1302,6 +1304,14 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
     if ((rc = dalloc_copy(&p->winv, winv))) return rc;
     if ((rc = dalloc_copy(&p->twN, twN))) return rc;
     if ((rc = dalloc_copy(&p->twP, twP))) return rc;
+    if (p->lds) {
+      std::vector<float2> tl(N);
+      for (int t = 0; t < N; ++t) {
+        const double ang = -2.0 * M_PI * (double)t / (double)N;
+        tl[t] = make_float2((float)cos(ang), (float)sin(ang));
+      }
+      if ((rc = dalloc_copy(&p->twL, tl))) return rc;
+    }
   }
   // --- limiter chunk descriptors, output prefix ---
   {
@@ -1386,7 +1396,9 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
   }
   // --- generic-hop scratch ---
   if (p->generic && p->total_frames > 0) {
-    if (hipMalloc(reinterpret_cast<void**>(&p->scratch), (size_t)p->total_frames * N * sizeof(cf)))
+    // register generic path: cf per position (L, R); any-size path: ch floats
+    const size_t per = p->lds ? (size_t)std::max(2, (int)d.ch) * sizeof(float) : sizeof(cf);
+    if (hipMalloc(reinterpret_cast<void**>(&p->scratch), (size_t)p->total_frames * N * per))
       return TOMATIS_E_NOMEM;
   }
   // --- min-hold workspace ---
@@ -1411,8 +1423,8 @@ int tomatis_plan_create(tomatis_plan_t* out, const TomatisPlanDesc* desc, const 
   if (!out || !desc || !window || (!streams && n_streams > 0) || n_streams < 0) return TOMATIS_E_ARG;
   *out = nullptr;
   const TomatisPlanDesc d = *desc;
-  if (d.n_fft != 2048 && d.n_fft != 4096) return TOMATIS_E_UNSUPPORTED;
-  if (d.ch < 1 || d.ch > 2) return TOMATIS_E_UNSUPPORTED;
+  if (d.n_fft < 256 || d.n_fft > 8192 || (d.n_fft & (d.n_fft - 1))) return TOMATIS_E_UNSUPPORTED;
+  if (d.ch < 1 || d.ch > 8) return TOMATIS_E_UNSUPPORTED;
   if (d.hop < 1 || d.hop > d.n_fft) return TOMATIS_E_ARG;
   if (d.up_delay_frames < 0 || d.up_delay_frames + 2 > kMaxGateStates) return TOMATIS_E_UNSUPPORTED;
   if (d.min_hold_frames < 0 || 2 * (d.min_hold_frames + 1) > 65535) return TOMATIS_E_UNSUPPORTED;
@@ -1425,11 +1437,14 @@ int tomatis_plan_create(tomatis_plan_t* out, const TomatisPlanDesc* desc, const 
   // (lanes P, registers NR) per transform: 2048 = 128 x 16, 4096 = 128 x 32
   // n_fft 2048: one wave per frame (P = 64, 32 registers, wave-local exchanges)
   // unless TOMATIS_P64=0; otherwise two waves per frame (P = 128)
-  p->P = (N == 2048 && env_int("TOMATIS_P64", 1)) ? 64 : 128;
+  // register kernels: n_fft 2048 / 4096 with <= 2 channels (L + iR); every
+  // other power of two in [256, 8192] or more channels: the any-size LDS path
+  p->lds = !(N == 2048 || N == 4096) || d.ch > 2 || env_int("TOMATIS_FORCE_LDS", 0) != 0;
+  p->P = p->lds ? 64 : ((N == 2048 && env_int("TOMATIS_P64", 1)) ? 64 : 128);
   p->NR = N / p->P;
-  p->SH = (hop % p->P == 0) ? hop / p->P : 0;
-  p->generic = p->NR == 16 ? !(p->SH == 2 || p->SH == 4 || p->SH == 8)
-                           : !(p->SH == 4 || p->SH == 8 || p->SH == 16);
+  p->SH = (!p->lds && hop % p->P == 0) ? hop / p->P : 0;
+  p->generic = p->lds || (p->NR == 16 ? !(p->SH == 2 || p->SH == 4 || p->SH == 8)
+                                      : !(p->SH == 4 || p->SH == 8 || p->SH == 16));
   for (int i = 0; i < n_streams && !p->generic; ++i) {
     const TomatisStream& s = streams[i];
     if (s.n_chunks > 1 && (((s.chunk_first - s.first_start) % hop) != 0 || (s.chunk_len % hop) != 0))
@@ -1668,6 +1683,36 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
   if (p->n_runs == 0) return TOMATIS_OK;
   hipStream_t s = (hipStream_t)hs;
   const int N = p->d.n_fft;
+  if (p->lds) {
+    LdsArgs L;
+    L.x = x;
+    L.st = p->st;
+    L.n_streams = p->n_streams;
+    L.gains = gains;
+    L.rows = rows;
+    L.win = p->win;
+    L.win2 = p->win2;
+    L.tw = p->twL;
+    L.scratch = reinterpret_cast<float*>(p->scratch);
+    L.y = y;
+    L.peaks = peaks;
+    L.pos_base = p->pos_base;
+    L.total_frames = p->total_frames;
+    L.total_out = p->total_out;
+    L.n_fft = N;
+    L.hop = p->d.hop;
+    L.ch = p->d.ch;
+    L.n_bins = N / 2 + 1;
+    L.norm_mode = p->d.norm_mode;
+    if (p->total_frames > 0) {
+      launch_lds_frames(L, s);
+      const int rc = launch_check();
+      if (rc) return rc;
+    }
+    if (p->total_out == 0) return TOMATIS_OK;
+    launch_lds_gather(L, s);
+    return launch_check();
+  }
   if (n_rows > p->gperm_rows) {  // grows only; reuse across calls (graph-safe after first call)
     dfree(p->gperm);
     p->gperm = nullptr;

@@ -54,6 +54,28 @@ struct MainArgs {
   unsigned long long* prof;  // TM_PROFILE builds only: per-phase wave cycles
 };
 
+// Any-size path (n_fft a power of two in [256, 8192], any hop, 1..8 channels):
+// per (frame, channel pair) an LDS Stockham FFT, windowed frames to scratch
+// float [frame][n_fft][ch], then a per-position gather in frame order.
+struct LdsArgs {
+  const float* x;
+  const TomatisStream* st;
+  int n_streams;
+  const float* gains;   // [rows][n_fft/2+1] natural bin order (the caller's table)
+  const uint16_t* rows;
+  const float* win;     // [N]
+  const float* win2;    // [N]
+  const float2* tw;     // [N] exp(-2 pi i t / N)
+  float* scratch;       // [total_frames][N][ch]
+  float* y;
+  uint32_t* peaks;
+  const int64_t* pos_base;  // output position prefix per stream
+  int64_t total_frames, total_out;
+  int n_fft, hop, ch, n_bins, norm_mode;
+};
+void launch_lds_frames(const LdsArgs& A, hipStream_t s);
+void launch_lds_gather(const LdsArgs& A, hipStream_t s);
+
 // launchers (tm_transform.hip); kernels stay private to that unit
 int transform_wg(int P, int NR);  // workgroup size of the fused kernel
 int transform_slots_per_cu(int P, int NR);  // resident sequences per CU

@@ -10,6 +10,7 @@
 
 #include "tm_common.h"
 #include "tm_fft.h"
+#include "tm_lds_fft.h"
 #include "tm_shared.h"
 
 using namespace tdsp;
@@ -713,6 +714,110 @@ __global__ __launch_bounds__(256) void k_ola_gather(MainArgs A, int n_streams,
 }
 
 
+// ---------------------------------------------------------------------------
+// Any-size path: n_fft a power of two in [256, 8192], any hop, 1..8 channels
+// (the register kernels above cover n_fft 2048 / 4096 with <= 2 channels).
+// Reference: the same per-frame filter, src/process_tomatis.py:394-406 (and the
+// adaptive :298-327 / layer2 :155-198 copies).  Workgroup = (frame, channel
+// pair c0, c1): frame of (x*in_scale)*win packed as c0 + i c1, forward FFT in
+// LDS, real even gain row (1/N folded in), inverse as conj(FFT(conj(.))),
+// synthesis window, to scratch; the OLA is a per-position gather below.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int stream_of_frame(const TomatisStream* st, int n, int64_t fg) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {  // last stream whose frame_base <= fg (empty streams share a base)
+    const int mid = (lo + hi + 1) / 2;
+    if (st[mid].frame_base <= fg) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+template <int N>
+__global__ __launch_bounds__(256) void k_stft_lds(LdsArgs A) {
+  __shared__ float2 buf[N];
+  const int64_t fg = blockIdx.x;
+  const TomatisStream S = A.st[stream_of_frame(A.st, A.n_streams, fg)];
+  const int64_t k = fg - S.frame_base;
+  const int64_t s_k = S.first_start + k * A.hop;
+  const int ch = A.ch, c0 = 2 * blockIdx.y, c1 = c0 + 1;
+  const bool has1 = c1 < ch;
+  const float* xs = A.x + S.in_off;
+  const float isc = S.in_scale;
+  for (int i = threadIdx.x; i < N; i += 256) {
+    const int64_t p = s_k + i;
+    const bool in = p >= 0 && p < S.n;
+    float a = in ? xs[p * ch + c0] : 0.f;
+    float b = (in && has1) ? xs[p * ch + c1] : 0.f;
+    const float w = A.win[i];
+    a = (a * isc) * w;  // x * in_scale first, then the window: two roundings as the reference
+    b = (b * isc) * w;
+    buf[i] = make_float2(a, b);
+  }
+  __syncthreads();
+  tlds::lds_fft<N>(buf, A.tw);
+  const uint16_t row = A.rows[S.frame_base + k];
+  const float* g = A.gains + (int64_t)row * A.n_bins;
+  constexpr float inv_n = 1.0f / (float)N;  // exact (power of two)
+  for (int b = threadIdx.x; b < N; b += 256) {
+    const float gk = g[b <= N / 2 ? b : N - b] * inv_n;
+    const float2 v = buf[b];
+    buf[b] = make_float2(v.x * gk, -(v.y * gk));  // conj for the inverse
+  }
+  __syncthreads();
+  tlds::lds_fft<N>(buf, A.tw);
+  float* out = A.scratch + fg * (int64_t)N * ch;
+  for (int i = threadIdx.x; i < N; i += 256) {
+    const float2 v = buf[i];
+    const float w = A.win[i];
+    out[(int64_t)i * ch + c0] = v.x * w;
+    if (has1) out[(int64_t)i * ch + c1] = -v.y * w;
+  }
+}
+
+// OLA gather of the any-size path: one thread per output position, all
+// channels; frames summed in ascending order (the reference's accumulation
+// order), sum w^2 likewise, normalise, output scale, chunk peak.
+__global__ __launch_bounds__(256) void k_ola_gather_lds(LdsArgs A) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= A.total_out) return;
+  int lo = 0, hi = A.n_streams - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) / 2;
+    if (A.pos_base[mid] <= t) lo = mid;
+    else hi = mid - 1;
+  }
+  const TomatisStream S = A.st[lo];
+  const int64_t p = S.out_begin + (t - A.pos_base[lo]);
+  const int hop = A.hop, N = A.n_fft, ch = A.ch;
+  const int64_t rel = p - S.first_start;
+  int64_t jhi = floordiv(rel, hop);
+  if (jhi > S.n_frames - 1) jhi = S.n_frames - 1;
+  int64_t jlo = floordiv(rel - N, hop) + 1;
+  if (jlo < 0) jlo = 0;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float w = 0.f;
+  for (int64_t j = jlo; j <= jhi; ++j) {
+    const int off = (int)(rel - j * hop);
+    const float* src = A.scratch + ((S.frame_base + j) * (int64_t)N + off) * ch;
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      if (c < ch) acc[c] = acc[c] + src[c];
+    w = w + A.win2[off];
+  }
+  const float d = norm_den(w, A.norm_mode);
+  float* ys = A.y + S.out_off + (p - S.out_begin) * ch;
+  float mag = 0.f;
+#pragma unroll
+  for (int c = 0; c < 8; ++c)
+    if (c < ch) {
+      const float o = (acc[c] / d) * S.out_scale;
+      ys[c] = o;
+      mag = fmaxf(mag, fabsf(o));
+    }
+  if (mag > 0.f) atomicMax(A.peaks + S.chunk_base + chunk_of(p, S), __float_as_uint(mag));
+}
+
 template <int P, int NR, int SH, bool PF, bool NT, int WG>
 void launch_main_pf(const MainArgs& A, int ch, hipStream_t s) {
   const bool gl = A.n_rows_lds > 0;
@@ -816,6 +921,19 @@ void launch_gain_perm(int P, int NR, const float* gains, int n_rows, int n_bins,
     hipLaunchKernelGGL((k_gain_perm<128, 16>), dim3(nb), dim3(256), 0, s, gains, n_rows, n_bins, out);
   else
     hipLaunchKernelGGL((k_gain_perm<128, 32>), dim3(nb), dim3(256), 0, s, gains, n_rows, n_bins, out);
+}
+
+void launch_lds_frames(const LdsArgs& A, hipStream_t s) {
+  const dim3 g((unsigned)A.total_frames, (unsigned)((A.ch + 1) / 2));
+#define LDS_N(NN) \
+  if (A.n_fft == NN) hipLaunchKernelGGL((k_stft_lds<NN>), g, dim3(256), 0, s, A);
+  LDS_N(256) LDS_N(512) LDS_N(1024) LDS_N(2048) LDS_N(4096) LDS_N(8192)
+#undef LDS_N
+}
+
+void launch_lds_gather(const LdsArgs& A, hipStream_t s) {
+  const int64_t ng = (A.total_out + 255) / 256;
+  hipLaunchKernelGGL(k_ola_gather_lds, dim3((unsigned)ng), dim3(256), 0, s, A);
 }
 
 void launch_ola_gather(const MainArgs& A, int n_streams, const int64_t* pos_base, int64_t total,

@@ -237,12 +237,15 @@ def _alloc_out(torch, lens, ch, device):
 
 
 def _check_fft(n_fft, hop, ch):
-    if n_fft not in (2048, 4096):
-        raise ValueError(f"n_fft={n_fft}: the gfx950 kernels are built for n_fft 2048 and 4096")
+    """Shapes the gfx950 library takes: register kernels for n_fft 2048 / 4096
+    with <= 2 channels, the any-size LDS path for every other power of two in
+    [256, 8192] and for 3..8 channels (tm_transform.hip)."""
+    if not (256 <= n_fft <= 8192) or (n_fft & (n_fft - 1)):
+        raise ValueError(f"n_fft={n_fft}: the gfx950 kernels take powers of two in [256, 8192]")
     if not (1 <= hop <= n_fft):
         raise ValueError(f"hop={hop} must be in [1, n_fft]")
-    if ch not in (1, 2):
-        raise ValueError(f"{ch} channels: the gfx950 kernels handle mono and stereo")
+    if not (1 <= ch <= 8):
+        raise ValueError(f"{ch} channels: the gfx950 kernels handle 1 to 8 channels")
 
 
 # ---------------------------------------------------------------------------
