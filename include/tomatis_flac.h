@@ -49,6 +49,28 @@ int tomatis_flac_info(const uint8_t* data, int64_t len, int32_t* sr, int32_t* ch
 int tomatis_flac_decode(const uint8_t* data, int64_t len, int32_t* pcm, int64_t max_frames,
                         int64_t* frames_out);
 
+/* Streaming encoder (the output side of a file pipeline: segments of PCM are
+ * pushed as they arrive from the device and encoded on host threads while the
+ * next segment is in flight).  Every push but the last must hold a multiple of
+ * 4096 frames; finish returns the complete stream (free with
+ * tomatis_flac_free), byte-identical to tomatis_flac_encode of the whole PCM. */
+typedef struct tomatis_flac_enc_s* tomatis_flac_enc_t;
+int tomatis_flac_enc_open(int32_t ch, int32_t sr, int32_t bps, tomatis_flac_enc_t* out);
+int tomatis_flac_enc_push(tomatis_flac_enc_t enc, const int32_t* pcm, int64_t frames);
+int tomatis_flac_enc_finish(tomatis_flac_enc_t enc, uint8_t** out, int64_t* out_len);
+void tomatis_flac_enc_close(tomatis_flac_enc_t enc);
+
+/* Byte offset of the first audio frame (after the metadata blocks), or -1. */
+int64_t tomatis_flac_first_frame(const uint8_t* data, int64_t len);
+
+/* Decode the frames whose first byte lies in [lo, hi) into pcm at their own
+ * sample offsets (pcm holds the whole stream, [max_frames][ch]); [*s_lo, *s_hi)
+ * = the samples written.  Consecutive byte ranges give consecutive sample
+ * ranges: the input side of a file pipeline uploads each range while the next
+ * one decodes. */
+int tomatis_flac_decode_bytes(const uint8_t* data, int64_t len, int64_t lo, int64_t hi,
+                              int32_t* pcm, int64_t max_frames, int64_t* s_lo, int64_t* s_hi);
+
 #ifdef __cplusplus
 }
 #endif

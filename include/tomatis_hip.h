@@ -227,6 +227,13 @@ int tomatis_absmax_streams(tomatis_plan_t plan, const float* x, uint32_t* out_bi
 /* y[i] = x[i] * scale (float32), n floats (layer-2 gain-protect copy). */
 int tomatis_scale_copy(const float* x, float* y, int64_t n, float scale, void* hip_stream);
 
+/* File-boundary sample conversion (libsndfile's
+ * normalisation, src/process_tomatis.py:225-251 reads float32 and writes
+ * PCM_24): out = pcm / 2^(bps-1) (float32, correctly rounded), and
+ * out = clip(rint(x * (2^(bps-1) - 1)), -2^(bps-1), 2^(bps-1) - 1). */
+int tomatis_pcm_to_float(const int32_t* pcm, int64_t n, int32_t bps, float* out, void* hip_stream);
+int tomatis_float_to_pcm(const float* x, int64_t n, int32_t bps, int32_t* out, void* hip_stream);
+
 /* Deterministic synthetic PCM (twin of tomatis_audio_processor_amd/synth.py):
  * samples [start, start+n) of stream `seed`, ch channels, interleaved. */
 int tomatis_synth_fill(float* x, int64_t n, int32_t ch, int32_t sr, uint32_t seed,

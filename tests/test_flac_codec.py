@@ -305,3 +305,56 @@ def test_corrupt_last_frame_of_unknown_total_is_an_error():
     b[len(b) - 1] ^= 0x10          # frame CRC-16 of a frame that starts with a sync code
     with pytest.raises(audio_io.AudioFormatError):
         audio_io.flac_decode_int(bytes(b))
+
+
+def test_streaming_encoder_byte_identical():
+    """Segments pushed to the streaming encoder (whole 4096-blocks, short last
+    push) give exactly the whole-buffer stream (fileio egress)."""
+    import ctypes as C
+    from tomatis_audio_processor_amd import fileio
+    h = fileio._flac()
+    rng = np.random.default_rng(8)
+    for n, ch, segs in ((4096 * 10 + 123, 2, [4096 * 3, 4096 * 3, 4096 * 4 + 123]),
+                        (4096 * 5, 1, [4096 * 5]), (77, 2, [77])):
+        x = rng.integers(-(1 << 23), 1 << 23, size=(n, ch)).astype(np.int32)
+        whole = audio_io.flac_encode_int(x, 48000, 24)
+        enc = C.c_void_p()
+        assert h.tomatis_flac_enc_open(ch, 48000, 24, C.byref(enc)) == 0
+        a = 0
+        for m in segs:
+            seg = np.ascontiguousarray(x[a:a + m])
+            assert h.tomatis_flac_enc_push(enc, seg.ctypes.data, m) == 0
+            a += m
+        out = C.POINTER(C.c_uint8)()
+        ln = C.c_int64()
+        assert h.tomatis_flac_enc_finish(enc, C.byref(out), C.byref(ln)) == 0
+        blob = C.string_at(out, ln.value)
+        h.tomatis_flac_free(out)
+        h.tomatis_flac_enc_close(enc)
+        assert blob == whole
+
+
+def test_byte_range_decode_reassembles():
+    """Consecutive byte ranges decode to consecutive sample ranges covering the
+    stream (fileio ingest), for several range counts."""
+    import ctypes as C
+    from tomatis_audio_processor_amd import fileio
+    h = fileio._flac()
+    rng = np.random.default_rng(9)
+    n, ch = 4096 * 37 + 1000, 2
+    x = rng.integers(-30000, 30000, size=(n, ch)).astype(np.int32)
+    blob = audio_io.flac_encode_int(x, 44100, 16)
+    first = h.tomatis_flac_first_frame(blob, len(blob))
+    assert first == 42
+    for K in (1, 3, 8, 50):
+        pcm = np.zeros((n, ch), np.int32)
+        edges = np.linspace(first, len(blob), K + 1).astype(np.int64)
+        got = 0
+        lo, hi = C.c_int64(), C.c_int64()
+        for k in range(K):
+            assert h.tomatis_flac_decode_bytes(blob, len(blob), int(edges[k]), int(edges[k + 1]),
+                                               pcm.ctypes.data, n, C.byref(lo), C.byref(hi)) == 0
+            if hi.value > lo.value:
+                assert lo.value == got
+                got = hi.value
+        assert got == n and np.array_equal(pcm, x)

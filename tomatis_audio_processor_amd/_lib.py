@@ -89,6 +89,8 @@ _SIGS = {
     "tomatis_scale_copy": (C.c_int, [_P, _P, C.c_int64, C.c_float, _P]),
     "tomatis_synth_fill": (C.c_int, [_P, C.c_int64, C.c_int32, C.c_int32, C.c_uint32,
                                      C.c_int64, _P]),
+    "tomatis_pcm_to_float": (C.c_int, [_P, C.c_int64, C.c_int32, _P, _P]),
+    "tomatis_float_to_pcm": (C.c_int, [_P, C.c_int64, C.c_int32, _P, _P]),
     # analysis spectra
     "tomatis_an_frame_r": (C.c_int, [_P, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                      C.c_float, _P, _P]),

@@ -63,9 +63,15 @@ def run(args):
     os.makedirs(args.out_dir, exist_ok=True)
     recs = []
     params = dict(n_fft=args.n_fft, hop=args.hop)
+    from . import fileio
     for (sr, ch), ids in sorted(groups.items()):
-        xs = [audio_io.read(args.input[i])[0] for i in ids]
-        ss = engine.StreamSet.from_arrays(xs, sr)
+        # files decoded into HBM (fileio: FLAC via page-locked ranges, int -> float on device)
+        parts = [fileio.read_device(args.input[i]) for i in ids]
+        x = torch.cat([p[0] for p in parts]) if parts else torch.zeros(1, device="cuda")
+        lens = [p[1] for p in parts]
+        offs = list(np.cumsum([0] + [n * ch for n in lens[:-1]]).astype(int))
+        del parts
+        ss = engine.StreamSet(x=x, offs=offs, lens=lens, ch=ch, sr=sr)
         if args.mode == "adaptive":
             pipe = engine.AdaptivePipeline(ss, **params)
         elif args.mode == "xfade":
@@ -81,7 +87,9 @@ def run(args):
             if args.out_ext == "wav":
                 audio_io.write(out, res.output(j), sr, "WAV", "PCM_24")
             else:
-                audio_io.write_with_fallback(out, res.output(j), sr, log=lambda m: None)
+                a = res.out_offs[j]
+                fileio.write_device(out, res.y[a:a + res.out_lens[j] * ch], res.out_lens[j], ch,
+                                    sr, log=lambda m: None)
         recs.append(sharding.stream_records(res, ids, rank))
     rec = np.concatenate(recs) if recs else np.zeros((0, sharding.REC), np.int64)
     dev = "cuda" if (ws > 1 and torch.cuda.is_available()) else None

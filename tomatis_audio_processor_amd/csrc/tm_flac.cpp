@@ -346,8 +346,9 @@ struct EncStats {
   int rc = TOMATIS_FLAC_OK;
 };
 
-void encode_blocks(const int32_t* pcm, int64_t frames, int ch, int bps, int64_t b0, int64_t b1,
-                   BitWriter& w, EncStats& st) {
+// pcm holds frames [base, base + ...) of the stream (streaming encoder segments)
+void encode_blocks(const int32_t* pcm, int64_t base, int64_t frames, int ch, int bps, int64_t b0,
+                   int64_t b1, BitWriter& w, EncStats& st) {
   const int64_t lim = bps == 32 ? INT32_MAX : (1ll << (bps - 1)) - 1;
   std::vector<int64_t> s[8], side, mid, res;
   uint32_t& min_fs = st.min_fs;
@@ -361,7 +362,7 @@ void encode_blocks(const int32_t* pcm, int64_t frames, int ch, int bps, int64_t 
     for (int c = 0; c < ch; ++c) {
       s[c].resize(n);
       for (int i = 0; i < n; ++i) {
-        const int64_t v = pcm[(f0 + i) * ch + c];
+        const int64_t v = pcm[(f0 - base + i) * ch + c];
         if (v > lim || v < -lim - 1) {
           st.rc = TOMATIS_FLAC_E_ARG;
           return;
@@ -453,7 +454,7 @@ void encode_blocks(const int32_t* pcm, int64_t frames, int ch, int bps, int64_t 
 // otherwise).  *consumed = frame bytes, *end = offset + block size.
 int decode_frame(const uint8_t* d, size_t len, size_t p, int ch0, int bps0, int64_t nominal,
                  int32_t* pcm, int64_t max_frames, std::vector<int64_t>* sub, size_t* consumed,
-                 int64_t* end) {
+                 int64_t* end, int64_t* start = nullptr) {
   const Crc& C = crc();
   BitReader r(d + p, len - p);
   if (r.get(14) != 0x3FFE) return TOMATIS_FLAC_E_FORMAT;
@@ -596,6 +597,7 @@ int decode_frame(const uint8_t* d, size_t len, size_t p, int ch0, int bps0, int6
   }
   *consumed = fbytes + 2;
   *end = off + n;
+  if (start) *start = off;
   return TOMATIS_FLAC_OK;
 }
 
@@ -623,20 +625,23 @@ bool no_frame_after(const uint8_t* d, size_t len, size_t p, int ch0, int bps0, i
 // that starts with a sync code and fails its CRC stays an error.
 void decode_range(const uint8_t* d, size_t len, size_t lo, size_t hi, bool exact_start, int ch0,
                   int bps0, int64_t nominal, int64_t total, int32_t* pcm, int64_t max_frames,
-                  int* rc, int64_t* end) {
+                  int* rc, int64_t* end, int64_t* begin = nullptr) {
   std::vector<int64_t> sub[8];
   size_t p = lo;
   *rc = TOMATIS_FLAC_OK;
   *end = 0;
+  if (begin) *begin = INT64_MAX;
   if (!exact_start) {
     while (true) {
       while (p + 1 < hi && !(d[p] == 0xFF && (d[p + 1] & 0xFE) == 0xF8)) ++p;
       if (p + 1 >= hi) return;  // no frame starts in this range
       size_t used;
       int64_t e;
-      if (decode_frame(d, len, p, ch0, bps0, nominal, pcm, max_frames, sub, &used, &e) ==
+      int64_t b;
+      if (decode_frame(d, len, p, ch0, bps0, nominal, pcm, max_frames, sub, &used, &e, &b) ==
           TOMATIS_FLAC_OK) {
         *end = std::max(*end, e);
+        if (begin) *begin = std::min(*begin, b);
         p += used;
         break;
       }
@@ -646,7 +651,8 @@ void decode_range(const uint8_t* d, size_t len, size_t lo, size_t hi, bool exact
   while (p < hi && p + 2 <= len) {
     size_t used;
     int64_t e;
-    const int r = decode_frame(d, len, p, ch0, bps0, nominal, pcm, max_frames, sub, &used, &e);
+    int64_t b;
+    const int r = decode_frame(d, len, p, ch0, bps0, nominal, pcm, max_frames, sub, &used, &e, &b);
     if (r) {
       const bool sync = d[p] == 0xFF && (d[p + 1] & 0xFE) == 0xF8;
       if ((total > 0 && *end >= total) ||
@@ -656,6 +662,7 @@ void decode_range(const uint8_t* d, size_t len, size_t lo, size_t hi, bool exact
       return;
     }
     *end = std::max(*end, e);
+    if (begin) *begin = std::min(*begin, b);
     p += used;
   }
 }
@@ -680,9 +687,9 @@ int tomatis_flac_encode(const int32_t* pcm, int64_t frames, int32_t ch, int32_t 
   for (int t = 0; t < nt; ++t) {
     const int64_t b0 = nblk * t / nt, b1 = nblk * (t + 1) / nt;
     if (t == nt - 1)
-      encode_blocks(pcm, frames, ch, bps, b0, b1, ws[t], sts[t]);
+      encode_blocks(pcm, 0, frames, ch, bps, b0, b1, ws[t], sts[t]);
     else
-      th.emplace_back(encode_blocks, pcm, frames, ch, bps, b0, b1, std::ref(ws[t]),
+      th.emplace_back(encode_blocks, pcm, (int64_t)0, frames, ch, bps, b0, b1, std::ref(ws[t]),
                       std::ref(sts[t]));
   }
   for (auto& x : th) x.join();
@@ -733,6 +740,96 @@ int tomatis_flac_encode(const int32_t* pcm, int64_t frames, int32_t ch, int32_t 
 
 void tomatis_flac_free(uint8_t* p) { free(p); }
 
+struct tomatis_flac_enc_s {
+  int ch = 0, sr = 0, bps = 0;
+  int64_t frames = 0;  // pushed so far (always a multiple of kBlock until the last push)
+  bool closed = false;
+  std::vector<uint8_t> body;
+  EncStats tot;
+};
+
+int tomatis_flac_enc_open(int32_t ch, int32_t sr, int32_t bps, tomatis_flac_enc_t* out) {
+  if (!out || ch < 1 || ch > 8 || sr < 1 || sr > 655350 || bps < 4 || bps > 32)
+    return TOMATIS_FLAC_E_ARG;
+  auto* e = new (std::nothrow) tomatis_flac_enc_s();
+  if (!e) return TOMATIS_FLAC_E_NOMEM;
+  e->ch = ch;
+  e->sr = sr;
+  e->bps = bps;
+  *out = e;
+  return TOMATIS_FLAC_OK;
+}
+
+int tomatis_flac_enc_push(tomatis_flac_enc_t e, const int32_t* pcm, int64_t frames) {
+  if (!e || frames < 0 || (frames > 0 && !pcm) || e->closed) return TOMATIS_FLAC_E_ARG;
+  if (frames == 0) return TOMATIS_FLAC_OK;
+  if (e->frames + frames >= (1ll << 36)) return TOMATIS_FLAC_E_ARG;
+  // blocks of this segment on host threads, appended in block order
+  const int64_t base = e->frames, end = base + frames;
+  const int64_t b0 = base / kBlock, b1 = (end + kBlock - 1) / kBlock;
+  const int64_t nblk = b1 - b0;
+  int nt = (int)std::min<int64_t>(std::max(1u, std::thread::hardware_concurrency()), 16);
+  if (const char* ev = getenv("TOMATIS_FLAC_THREADS")) nt = std::max(1, atoi(ev));
+  nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, nblk / 8));
+  std::vector<BitWriter> ws(nt);
+  std::vector<EncStats> sts(nt);
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t) {
+    const int64_t c0 = b0 + nblk * t / nt, c1 = b0 + nblk * (t + 1) / nt;
+    if (t == nt - 1)
+      encode_blocks(pcm, base, end, e->ch, e->bps, c0, c1, ws[t], sts[t]);
+    else
+      th.emplace_back(encode_blocks, pcm, base, end, e->ch, e->bps, c0, c1, std::ref(ws[t]),
+                      std::ref(sts[t]));
+  }
+  for (auto& x : th) x.join();
+  for (int t = 0; t < nt; ++t) {
+    if (sts[t].rc) return sts[t].rc;
+    e->tot.min_fs = std::min(e->tot.min_fs, sts[t].min_fs);
+    e->tot.max_fs = std::max(e->tot.max_fs, sts[t].max_fs);
+    e->tot.min_bs = std::min(e->tot.min_bs, sts[t].min_bs);
+    e->tot.max_bs = std::max(e->tot.max_bs, sts[t].max_bs);
+    e->body.insert(e->body.end(), ws[t].buf.begin(), ws[t].buf.end());
+  }
+  e->frames = end;
+  if (end % kBlock) e->closed = true;  // a short block ends the stream
+  return TOMATIS_FLAC_OK;
+}
+
+int tomatis_flac_enc_finish(tomatis_flac_enc_t e, uint8_t** out, int64_t* out_len) {
+  if (!e || !out || !out_len) return TOMATIS_FLAC_E_ARG;
+  const int64_t frames = e->frames;
+  uint32_t min_fs = e->tot.min_fs, max_fs = e->tot.max_fs;
+  int min_bs = e->tot.min_bs, max_bs = e->tot.max_bs;
+  if (frames == 0) min_fs = max_fs = 0, min_bs = max_bs = kBlock;
+  BitWriter si;
+  si.put(frames > kBlock ? kBlock : (uint32_t)std::max(16, min_bs), 16);
+  si.put(std::max(16, max_bs), 16);
+  si.put(min_fs, 24);
+  si.put(max_fs, 24);
+  si.put((uint32_t)e->sr, 20);
+  si.put(e->ch - 1, 3);
+  si.put(e->bps - 1, 5);
+  si.put((uint64_t)frames >> 32, 4);
+  si.put((uint64_t)frames & 0xFFFFFFFFu, 32);
+  for (int i = 0; i < 16; ++i) si.put(0, 8);
+  const size_t hdr = 4 + 4 + 34;
+  uint8_t* o = (uint8_t*)malloc(hdr + e->body.size());
+  if (!o) return TOMATIS_FLAC_E_NOMEM;
+  memcpy(o, "fLaC", 4);
+  o[4] = 0x80;
+  o[5] = 0;
+  o[6] = 0;
+  o[7] = 34;
+  memcpy(o + 8, si.buf.data(), 34);
+  if (!e->body.empty()) memcpy(o + hdr, e->body.data(), e->body.size());
+  *out = o;
+  *out_len = (int64_t)(hdr + e->body.size());
+  return TOMATIS_FLAC_OK;
+}
+
+void tomatis_flac_enc_close(tomatis_flac_enc_t e) { delete e; }
+
 int tomatis_flac_info(const uint8_t* d, int64_t len, int32_t* sr, int32_t* ch, int32_t* bps,
                       int64_t* frames) {
   if (!d || len < 42 || memcmp(d, "fLaC", 4) != 0) return TOMATIS_FLAC_E_FORMAT;
@@ -748,6 +845,67 @@ int tomatis_flac_info(const uint8_t* d, int64_t len, int32_t* sr, int32_t* ch, i
   if (ch) *ch = c;
   if (bps) *bps = b;
   if (frames) *frames = n;
+  return TOMATIS_FLAC_OK;
+}
+
+int64_t tomatis_flac_first_frame(const uint8_t* d, int64_t len) {
+  if (!d || len < 42 || memcmp(d, "fLaC", 4) != 0) return -1;
+  size_t p = 4;
+  while (true) {
+    if (p + 4 > (size_t)len) return -1;
+    const bool last = d[p] & 0x80;
+    const size_t bl = ((size_t)d[p + 1] << 16) | ((size_t)d[p + 2] << 8) | d[p + 3];
+    p += 4 + bl;
+    if (last) break;
+  }
+  return (int64_t)p;
+}
+
+int tomatis_flac_decode_bytes(const uint8_t* d, int64_t len, int64_t lo, int64_t hi,
+                              int32_t* pcm, int64_t max_frames, int64_t* s_lo, int64_t* s_hi) {
+  int32_t sr0, ch0, bps0;
+  int64_t total;
+  int rc = tomatis_flac_info(d, len, &sr0, &ch0, &bps0, &total);
+  if (rc) return rc;
+  const int64_t first = tomatis_flac_first_frame(d, len);
+  if (first < 0) return TOMATIS_FLAC_E_FORMAT;
+  if (!pcm || !s_lo || !s_hi || lo < 0 || hi < lo) return TOMATIS_FLAC_E_ARG;
+  lo = std::max(lo, first);
+  hi = std::min(hi, len);
+  *s_lo = *s_hi = 0;
+  if (hi <= lo) return TOMATIS_FLAC_OK;
+  const int64_t nominal = ((int64_t)d[10] << 8) | d[11];
+  const size_t body = (size_t)(hi - lo);
+  int nt = (int)std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), 16);
+  if (const char* e = getenv("TOMATIS_FLAC_THREADS")) nt = std::max(1, atoi(e));
+  nt = (int)std::max<size_t>(1, std::min<size_t>(nt, body / (1u << 18)));
+  std::vector<int> rcs(nt);
+  std::vector<int64_t> ends(nt), begs(nt);
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t) {
+    const size_t a = lo + body * t / nt, b = lo + body * (t + 1) / nt;
+    const bool exact = t == 0 && lo == first;
+    const size_t bhi = (t == nt - 1 && hi == len) ? (size_t)len : b;
+    if (t == nt - 1)
+      decode_range(d, (size_t)len, a, bhi, exact, ch0, bps0, nominal, total, pcm, max_frames,
+                   &rcs[t], &ends[t], &begs[t]);
+    else
+      th.emplace_back(decode_range, d, (size_t)len, a, bhi, exact, ch0, bps0, nominal, total, pcm,
+                      max_frames, &rcs[t], &ends[t], &begs[t]);
+  }
+  for (auto& x : th) x.join();
+  int64_t b = INT64_MAX, e = 0;
+  for (int t = 0; t < nt; ++t) {
+    if (rcs[t]) return rcs[t];
+    if (ends[t] > 0) {
+      e = std::max(e, ends[t]);
+      b = std::min(b, begs[t]);
+    }
+  }
+  if (e == 0) return TOMATIS_FLAC_OK;  // no frame starts in [lo, hi)
+  if (total) e = std::min(e, total);
+  *s_lo = std::min(b, max_frames);
+  *s_hi = std::min(e, max_frames);
   return TOMATIS_FLAC_OK;
 }
 
@@ -784,7 +942,7 @@ int tomatis_flac_decode(const uint8_t* d, int64_t len, int32_t* pcm, int64_t max
                    max_frames, &rcs[t], &ends[t]);
     else
       th.emplace_back(decode_range, d, (size_t)len, lo, hi, t == 0, ch0, bps0, nominal, total,
-                      pcm, max_frames, &rcs[t], &ends[t]);
+                      pcm, max_frames, &rcs[t], &ends[t], (int64_t*)nullptr);
   }
   for (auto& x : th) x.join();
   int64_t done = 0;

@@ -915,6 +915,28 @@ __global__ __launch_bounds__(256) void k_scale_copy(const float* __restrict__ x,
     y[i] = x[i] * s;
 }
 
+// PCM <-> float at the file boundary, libsndfile's
+// normalisation as audio_io implements it: int -> float divides by 2^(bps-1)
+// (correctly rounded: double division, then float); float -> int multiplies by
+// 2^(bps-1) - 1 in double, rounds half to even and clips to the bps range.
+__global__ __launch_bounds__(256) void k_pcm_to_float(const int32_t* __restrict__ pcm, int64_t n,
+                                                      double inv, float* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (float)((double)pcm[i] * inv);
+}
+
+__global__ __launch_bounds__(256) void k_float_to_pcm(const float* __restrict__ x, int64_t n,
+                                                      double scale, double lo, double hi,
+                                                      int32_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    double v = rint((double)x[i] * scale);
+    v = v < lo ? lo : (v > hi ? hi : v);
+    out[i] = (int32_t)v;
+  }
+}
+
 __device__ __forceinline__ uint32_t lowbias32(uint32_t v) {
   v ^= v >> 16;
   v *= 0x7FEB352Du;
@@ -1852,6 +1874,26 @@ int tomatis_scale_copy(const float* x, float* y, int64_t n, float scale, void* h
   if (n == 0) return TOMATIS_OK;
   const unsigned g = (unsigned)std::min<int64_t>(4096, (n + 1023) / 1024);
   hipLaunchKernelGGL(k_scale_copy, dim3(g), dim3(256), 0, (hipStream_t)hs, x, y, n, scale);
+  return launch_check();
+}
+
+int tomatis_pcm_to_float(const int32_t* pcm, int64_t n, int32_t bps, float* out, void* hs) {
+  if (!pcm || !out || n < 0 || bps < 2 || bps > 32) return TOMATIS_E_ARG;
+  if (n == 0) return TOMATIS_OK;
+  // x / 2^(bps-1): the reciprocal is a power of two, so the product is exact in double
+  const double inv = 1.0 / (double)(1ll << (bps - 1));
+  const unsigned g = (unsigned)std::min<int64_t>(8192, (n + 1023) / 1024);
+  hipLaunchKernelGGL(k_pcm_to_float, dim3(g), dim3(256), 0, (hipStream_t)hs, pcm, n, inv, out);
+  return launch_check();
+}
+
+int tomatis_float_to_pcm(const float* x, int64_t n, int32_t bps, int32_t* out, void* hs) {
+  if (!x || !out || n < 0 || bps < 2 || bps > 32) return TOMATIS_E_ARG;
+  if (n == 0) return TOMATIS_OK;
+  const double top = (double)((1ll << (bps - 1)) - 1);
+  const unsigned g = (unsigned)std::min<int64_t>(8192, (n + 1023) / 1024);
+  hipLaunchKernelGGL(k_float_to_pcm, dim3(g), dim3(256), 0, (hipStream_t)hs, x, n, top,
+                     -top - 1.0, top, out);
   return launch_check();
 }
 

@@ -1,0 +1,212 @@
+"""Streaming file ingest and egress for the device pipeline.
+
+The reference decodes with libsndfile in 10-s blocks and writes FLAC PCM_24
+chunk by chunk (src/process_tomatis.py:225-251,433-457).  Here a file goes
+straight between the native FLAC codec and HBM:
+
+ingest   FLAC bytes -> K byte ranges decoded on host threads into one
+         page-locked int32 block (``tomatis_flac_decode_bytes``); each range's
+         samples are DMA'd to HBM on a copy stream while the next range
+         decodes; int -> float32 (libsndfile's 2^(bps-1) rule) on the device.
+egress   float32 -> PCM_24 on the device (``tomatis_float_to_pcm``), then
+         segments of 2^20 frames D2H into two alternating page-locked
+         buffers on a copy stream, each encoded on host threads
+         (``tomatis_flac_enc_push``) while the next one is in flight; the
+         stream is byte-identical to a whole-buffer encode.
+
+WAV files (and any format when libsndfile is importable) go through
+``audio_io`` on the host as before; the reference's FLAC -> WAV fallback on an
+encoder failure is kept.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import time
+
+import numpy as np
+
+from . import audio_io
+from ._lib import check, lib, ptr, stream_handle
+
+SEG_FRAMES = 4096 * 256      # egress segment (a whole number of FLAC blocks)
+IN_RANGES = 8                # ingest byte ranges
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        raise RuntimeError("device file I/O needs a ROCm GPU (MI355X)")
+    return torch
+
+
+def _flac():
+    h = audio_io._flac()
+    if not getattr(h, "_tm_stream_sigs", False):
+        P, I32, I64 = C.c_void_p, C.c_int32, C.c_int64
+        h.tomatis_flac_enc_open.argtypes = [I32, I32, I32, C.POINTER(P)]
+        h.tomatis_flac_enc_push.argtypes = [P, P, I64]
+        h.tomatis_flac_enc_finish.argtypes = [P, C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(I64)]
+        h.tomatis_flac_enc_close.argtypes = [P]
+        h.tomatis_flac_enc_close.restype = None
+        h.tomatis_flac_first_frame.argtypes = [P, I64]
+        h.tomatis_flac_first_frame.restype = I64
+        h.tomatis_flac_decode_bytes.argtypes = [P, I64, I64, I64, P, I64, C.POINTER(I64),
+                                                C.POINTER(I64)]
+        h._tm_stream_sigs = True
+    return h
+
+
+def _err(rc, what):
+    if rc:
+        raise audio_io.AudioFormatError(f"{what}: {audio_io._FLAC_ERR.get(rc, rc)}")
+
+
+class Timer(dict):
+    """Wall-clock phases of one file (seconds), for the e2e bench."""
+
+    def add(self, k, t0):
+        self[k] = self.get(k, 0.0) + time.perf_counter() - t0
+
+
+def read_device(path: str, timer: Timer | None = None):
+    """(x float32 cuda tensor [n*ch] interleaved, n, ch, sr) of an audio file."""
+    torch = _torch()
+    kind = audio_io._sniff(path)
+    if kind == "flac" and not audio_io.have_soundfile():
+        return _read_flac_device(path, timer)
+    t0 = time.perf_counter()
+    x, sr = audio_io.read(path)
+    if timer is not None:
+        timer.add("decode", t0)
+    t0 = time.perf_counter()
+    n, ch = x.shape
+    xd = torch.from_numpy(np.ascontiguousarray(x).reshape(-1)).cuda()
+    if timer is not None:
+        torch.cuda.synchronize()
+        timer.add("h2d", t0)
+    return xd, n, ch, sr
+
+
+def _read_flac_device(path, timer=None):
+    torch = _torch()
+    h = _flac()
+    t0 = time.perf_counter()
+    data = audio_io._flac_bytes(path)
+    if timer is not None:
+        timer.add("read", t0)
+    sr, ch, bps, n = audio_io.flac_info_bytes(data)
+    if n == 0:
+        n = audio_io.flac_count_frames(data)
+    buf = data
+    pin = torch.empty(max(1, n * ch), dtype=torch.int32, pin_memory=True)
+    dev = torch.empty(max(1, n * ch), dtype=torch.int32, device="cuda")
+    cs = torch.cuda.Stream()
+    first = int(h.tomatis_flac_first_frame(buf, len(data)))
+    if first < 0:
+        raise audio_io.AudioFormatError(f"{path}: not a FLAC stream")
+    edges = np.linspace(first, len(data), IN_RANGES + 1).astype(np.int64)
+    s_lo, s_hi = C.c_int64(), C.c_int64()
+    got = 0
+    t0 = time.perf_counter()
+    for k in range(IN_RANGES):
+        _err(h.tomatis_flac_decode_bytes(buf, len(data), int(edges[k]), int(edges[k + 1]),
+                                         pin.data_ptr(), n, C.byref(s_lo), C.byref(s_hi)),
+             "FLAC decode failed")
+        a, b = s_lo.value, s_hi.value
+        if b > a:
+            if a != got:
+                raise audio_io.AudioFormatError(f"{path}: FLAC frames out of order / missing")
+            with torch.cuda.stream(cs):   # DMA while the next range decodes
+                dev[a * ch:b * ch].copy_(pin[a * ch:b * ch], non_blocking=True)
+            got = b
+    if got != n:
+        raise audio_io.AudioFormatError(f"{path}: decoded {got} of {n} frames")
+    torch.cuda.current_stream().wait_stream(cs)
+    x = torch.empty(max(1, n * ch), dtype=torch.float32, device="cuda")
+    check(lib().tomatis_pcm_to_float(ptr(dev), n * ch, bps, ptr(x), stream_handle()),
+          "pcm_to_float")
+    if timer is not None:
+        torch.cuda.synchronize()
+        timer.add("decode+h2d", t0)
+    cs.synchronize()   # the page-locked block may be reused once the copies have landed
+    return x[:n * ch], n, ch, sr
+
+
+def encode_flac_device(y, n: int, ch: int, sr: int, bps: int = 24, timer=None) -> bytes:
+    """FLAC stream of the device float32 samples y [n*ch] at ``bps`` bits."""
+    torch = _torch()
+    h = _flac()
+    t0 = time.perf_counter()
+    yi = torch.empty(max(1, n * ch), dtype=torch.int32, device="cuda")
+    check(lib().tomatis_float_to_pcm(ptr(y), n * ch, bps, ptr(yi), stream_handle()),
+          "float_to_pcm")
+    enc = C.c_void_p()
+    _err(h.tomatis_flac_enc_open(ch, sr, bps, C.byref(enc)), "FLAC encode failed")
+    try:
+        seg = SEG_FRAMES
+        K = (n + seg - 1) // seg
+        pins = [torch.empty(seg * ch, dtype=torch.int32, pin_memory=True)
+                for _ in range(min(2, max(1, K)))]
+        evs = [torch.cuda.Event() for _ in pins]
+        cs = torch.cuda.Stream()
+        cs.wait_stream(torch.cuda.current_stream())
+
+        def issue(k):
+            a, b = k * seg, min(n, (k + 1) * seg)
+            with torch.cuda.stream(cs):
+                pins[k % 2][:(b - a) * ch].copy_(yi[a * ch:b * ch], non_blocking=True)
+                evs[k % 2].record(cs)
+
+        if K:
+            issue(0)
+        for k in range(K):
+            if k + 1 < K:
+                issue(k + 1)          # its buffer's previous segment was pushed at k - 1
+            evs[k % 2].synchronize()
+            a, b = k * seg, min(n, (k + 1) * seg)
+            _err(h.tomatis_flac_enc_push(enc, pins[k % 2].data_ptr(), b - a),
+                 "FLAC encode failed")
+        out = C.POINTER(C.c_uint8)()
+        ln = C.c_int64()
+        _err(h.tomatis_flac_enc_finish(enc, C.byref(out), C.byref(ln)), "FLAC encode failed")
+        try:
+            blob = C.string_at(out, ln.value)
+        finally:
+            h.tomatis_flac_free(out)
+    finally:
+        h.tomatis_flac_enc_close(enc)
+    if timer is not None:
+        timer.add("d2h+encode", t0)
+    return blob
+
+
+def write_device(out_path: str, y, n: int, ch: int, sr: int, log=print, timer=None):
+    """FLAC PCM_24 of device samples y [n*ch], else the reference's WAV fallback
+    at ``out_path.replace('.flac', '.wav')`` (src/process_tomatis.py:242-251).
+    Returns (written_path, is_flac)."""
+    if audio_io.have_soundfile():
+        return audio_io.write_with_fallback(out_path, y.cpu().numpy().reshape(n, ch), sr, log=log)
+    try:
+        blob = encode_flac_device(y, n, ch, sr, 24, timer)
+        t0 = time.perf_counter()
+        with open(out_path, "wb") as f:
+            f.write(blob)
+        if timer is not None:
+            timer.add("write", t0)
+        log("[OK] 输出格式: FLAC 24-bit")
+        return out_path, True
+    except Exception as e:
+        log(f"[WARN] FLAC 写入失败: {e}")
+        wav_path = out_path.replace(".flac", ".wav")
+        audio_io.write(wav_path, y.cpu().numpy().reshape(n, ch), sr, "WAV", "PCM_24")
+        log("[OK] 输出格式: WAV 24-bit (稍后需转换为 FLAC)")
+        return wav_path, False
+
+
+def device_stream_set(x, n: int, ch: int, sr: int):
+    """One-stream ``engine.StreamSet`` over a device buffer from read_device."""
+    from . import engine
+    return engine.StreamSet(x=x, offs=[0], lens=[n], ch=ch, sr=sr)
+
+
+__all__ = ["read_device", "write_device", "encode_flac_device", "device_stream_set", "Timer"]

@@ -23,17 +23,17 @@ def db_to_lin(db):
 
 
 def run_residual_eq(in_audio, out_audio, eq_lin, n_fft, hop):
-    from . import engine
+    from . import engine, fileio
     import torch
     sr, ch, _ = audio_io.info(in_audio)
     assert ch == 2, "只支持双声道"
-    x, sr = audio_io.read(in_audio)
-    ss = engine.StreamSet.from_arrays([x], sr)
+    x, n, ch, sr = fileio.read_device(in_audio)
+    ss = fileio.device_stream_set(x, n, ch, sr)
     pipe = engine.StaticEqPipeline(ss, eq_lin, n_fft=n_fft, hop=hop, pad=False)
     res = pipe.run()
     torch.cuda.synchronize()
-    y = res.output(0)
-    written, _ = audio_io.write_with_fallback(out_audio, y, sr, log=lambda m: None)
+    y = res.y[res.out_offs[0]:res.out_offs[0] + res.out_lens[0] * ch]
+    written, _ = fileio.write_device(out_audio, y, res.out_lens[0], ch, sr, log=lambda m: None)
     return written
 
 

@@ -47,6 +47,22 @@ def run_gate_file(x, sr, *, xfade_ms=None, **params):
     return res.output(0), res, pipe
 
 
+def run_gate_path(in_path, out_path, *, xfade_ms=None, timer=None, **params):
+    """File -> file through the device (fileio: FLAC decoded into page-locked
+    memory and streamed to HBM, PCM_24 quantised on the device and encoded
+    while the next segment is copied back).  Returns (result, written, is_flac, N)."""
+    from . import engine, fileio
+    import torch
+    x, n, ch, sr = fileio.read_device(in_path, timer)
+    ss = fileio.device_stream_set(x, n, ch, sr)
+    pipe = engine.GatePipeline(ss, xfade_ms=xfade_ms, **params)
+    res = pipe.run()
+    torch.cuda.synchronize()
+    y = res.y[res.out_offs[0]:res.out_offs[0] + res.out_lens[0] * ch]
+    written, is_flac = fileio.write_device(out_path, y, res.out_lens[0], ch, sr, timer=timer)
+    return res, written, is_flac, n
+
+
 def process(
     in_path,
     out_path,
@@ -84,16 +100,12 @@ def process(
     print(f"[OK] 采样率: {sr} Hz\n[OK] 声道数: {ch}\n[OK] 总长度: {frames} 采样点 "
           f"({frames / sr:.2f} 秒)")
     check_format(sr, ch, allow_any_format)
-    x, sr = audio_io.read(in_path)
-    N = len(x)
-
-    y, res, pipe = run_gate_file(
-        x, sr, gate_ui=gate_ui, gate_mode=gate_mode, dynamic_range=dynamic_range,
+    res, written, is_flac, N = run_gate_path(
+        in_path, out_path, gate_ui=gate_ui, gate_mode=gate_mode, dynamic_range=dynamic_range,
         gate_scale=gate_scale, gate_offset=gate_offset, hysteresis_db=hysteresis_db, fc=fc,
         slope=slope, c1_low=c1_low, c1_high=c1_high, c2_low=c2_low, c2_high=c2_high,
         up_delay_ms=up_delay_ms, n_fft=n_fft, hop=hop, output_gain_db=output_gain_db)
     states = res.stream_states(0)
-    written, is_flac = audio_io.write_with_fallback(out_path, y, sr)
 
     if state_csv_path:
         starts = res.first_start[0] + hop * np.arange(len(states), dtype=np.int64)

@@ -51,21 +51,20 @@ def process(
     state_csv_path=None,
 ):
     """Adaptive gate + cross-fade tilt processing of ``in_path`` -> ``out_path``."""
-    from . import engine
+    from . import engine, fileio
     import torch
     print("=" * 60 + "\nTomatis 自适应处理器 (MI355X)\n" + "=" * 60)
     print(f"\n读取输入: {in_path}")
-    x, sr = audio_io.read(in_path)
-    N, ch = x.shape
+    x, N, ch, sr = fileio.read_device(in_path)
     print(f"  采样率: {sr} Hz\n  声道数: {ch}\n  时长: {N / sr:.2f} s")
-    ss = engine.StreamSet.from_arrays([x], sr)
+    ss = fileio.device_stream_set(x, N, ch, sr)
     pipe = engine.AdaptivePipeline(ss, fc=fc, slope=slope, c1_low=c1_low, c1_high=c1_high,
                                    c2_low=c2_low, c2_high=c2_high, target_c2=target_c2,
                                    hyst_db=hyst_db, min_hold_ms=min_hold_ms, xfade_ms=xfade_ms,
                                    headroom_margin=headroom_margin, n_fft=n_fft, hop=hop)
     res = pipe.run()
     torch.cuda.synchronize()
-    y = res.output(0)
+    y_dev = res.y[res.out_offs[0]:res.out_offs[0] + res.out_lens[0] * ch]
     states = res.stream_states(0)
     alpha = res.stream_alpha(0)
     a = res.frame_base[0]
@@ -80,10 +79,11 @@ def process(
     print(f"\n预衰减: {-atten:.2f} dB\n  最优阈值 T: {T:.2f} dBFS\n  C2 占比: {c2_ratio * 100:.1f}%"
           f"\n  切换次数: {switches}")
     if out_path.lower().endswith(".wav"):
-        audio_io.write(out_path, y, sr, "WAV", "PCM_24")
+        audio_io.write(out_path, y_dev.cpu().numpy().reshape(-1, ch), sr, "WAV", "PCM_24")
         written = out_path
     else:  # reference: sf.write(out_path, y, sr, subtype='PCM_24')
-        written, _ = audio_io.write_with_fallback(out_path, y, sr, log=lambda m: None)
+        written, _ = fileio.write_device(out_path, y_dev, res.out_lens[0], ch, sr,
+                                         log=lambda m: None)
     print(f"\n输出已保存: {written}")
     if state_csv_path:
         frame_sec = hop / sr

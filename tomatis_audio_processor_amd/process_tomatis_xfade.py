@@ -14,7 +14,7 @@ import csv
 import numpy as np
 
 from . import audio_io, dsp
-from .process_tomatis import check_format, run_gate_file
+from .process_tomatis import check_format, run_gate_path
 
 EPS = dsp.EPS
 PEAK_LIMIT = dsp.PEAK_LIMIT
@@ -50,14 +50,11 @@ def process(
     sr, ch, frames = audio_io.info(in_path)
     print(f"✓ 采样率: {sr} Hz\n✓ 声道数: {ch}\n✓ 总长度: {frames} 采样点 ({frames / sr:.2f} 秒)")
     check_format(sr, ch, allow_any_format)
-    x, sr = audio_io.read(in_path)
-    N = len(x)
-    y, res, pipe = run_gate_file(
-        x, sr, xfade_ms=xfade_ms, gate_ui=gate_ui, gate_scale=gate_scale,
+    res, written, is_flac, N = run_gate_path(
+        in_path, out_path, xfade_ms=xfade_ms, gate_ui=gate_ui, gate_scale=gate_scale,
         gate_offset=gate_offset, hysteresis_db=hysteresis_db, fc=fc, slope=slope,
         c1_low=c1_low, c1_high=c1_high, c2_low=c2_low, c2_high=c2_high,
         up_delay_ms=up_delay_ms, n_fft=n_fft, hop=hop)
-    written, is_flac = audio_io.write_with_fallback(out_path, y, sr)
     states = res.stream_states(0)
     alpha = res.stream_alpha(0)
     if state_csv_path:

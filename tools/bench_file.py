@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""File -> file rates of the standard CLI path for C2 (one 60-min stereo
+44.1 kHz FLAC PCM_24 file, 2048/512): the device file path (fileio: ranged
+FLAC decode streamed to HBM, device PCM conversion, double-buffered D2H +
+streaming encode) against the host path of round 1 (audio_io.read ->
+StreamSet.from_arrays -> Result.output -> audio_io.write), and the codec
+alone.  One JSON line."""
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    from tomatis_audio_processor_amd import audio_io, engine, fileio
+    from tomatis_audio_processor_amd.process_tomatis import run_gate_path
+    secs = int(os.environ.get("BENCH_FILE_SECS", "3600"))
+    sr, ch = 44100, 2
+    n = secs * sr
+    params = dict(gate_ui=50, n_fft=2048, hop=512)
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as d:
+        src, out1, out2 = (os.path.join(d, f) for f in ("in.flac", "dev.flac", "host.flac"))
+        ss = engine.StreamSet.synthetic(1, n, ch, sr, seed0=1000)
+        blob = fileio.encode_flac_device(ss.x, n, ch, sr, 24)
+        with open(src, "wb") as f:
+            f.write(blob)
+        del ss
+        torch.cuda.synchronize()
+        # warm: pinned allocator, kernels, codec threads
+        run_gate_path(src, out1, **params)
+        runs = []
+        for _ in range(2):
+            tm = fileio.Timer()
+            t0 = time.perf_counter()
+            run_gate_path(src, out1, timer=tm, **params)
+            torch.cuda.synchronize()
+            tm["total"] = time.perf_counter() - t0
+            runs.append(tm)
+        dev = min(runs, key=lambda t: t["total"])
+        # round-1 host path
+        t0 = time.perf_counter()
+        x, _ = audio_io.read(src)
+        t_read = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        s2 = engine.StreamSet.from_arrays([x], sr)
+        pipe = engine.GatePipeline(s2, **params)
+        res = pipe.run()
+        y = res.output(0)
+        t_mid = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        audio_io.write(out2, y, sr, "FLAC", "PCM_24")
+        t_write = time.perf_counter() - t0
+        same = open(out1, "rb").read() == open(out2, "rb").read()
+        # codec alone on the same PCM
+        v = np.clip(np.rint(y.astype(np.float64) * 8388607.0), -8388608, 8388607).astype(np.int32)
+        t0 = time.perf_counter()
+        b2 = audio_io.flac_encode_int(v, sr, 24)
+        t_enc = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        audio_io.flac_decode_int(b2)
+        t_dec = time.perf_counter() - t0
+    S = n * ch / 1e6
+    host_total = t_read + t_mid + t_write
+    print(json.dumps({
+        "workload": f"C2 file->file: {secs} s stereo 44.1 kHz FLAC PCM_24, standard 2048/512",
+        "device_path_s": {k: round(v, 3) for k, v in dev.items()},
+        "device_path_msamples_s": round(S / dev["total"], 1),
+        "host_path_s": {"read": round(t_read, 3), "upload+run+download": round(t_mid, 3),
+                        "write": round(t_write, 3), "total": round(host_total, 3)},
+        "host_path_msamples_s": round(S / host_total, 1),
+        "outputs_byte_identical": same,
+        "flac_encode_s": round(t_enc, 3), "flac_decode_s": round(t_dec, 3),
+        "encoder_bound_msamples_s": round(S / t_enc, 1),
+        "device_path_over_encoder_bound": round(dev["total"] / t_enc, 3),
+    }), flush=True)
+
+
+if __name__ == "__main__":
+    main()
