@@ -73,7 +73,7 @@ def process(
     print(f"\n统计信息:\n  总帧数: {F}\n  C1 帧数: {c1} ({c1 / F * 100:.1f}%)")
     print(f"  C2 帧数: {F - c1} ({(F - c1) / F * 100:.1f}%)")
     if xfade_ms > 0:
-        print(f"  Crossfade: {xfade_ms} ms ({pipe.xf} 帧)")
+        print(f"  Crossfade: {xfade_ms} ms ({res.extra['xfade_frames']} 帧)")
     print(f"\n输出文件: {written}")
     return None
 
