@@ -58,6 +58,11 @@ typedef struct tomatis_flac_enc_s* tomatis_flac_enc_t;
 int tomatis_flac_enc_open(int32_t ch, int32_t sr, int32_t bps, tomatis_flac_enc_t* out);
 int tomatis_flac_enc_push(tomatis_flac_enc_t enc, const int32_t* pcm, int64_t frames);
 int tomatis_flac_enc_finish(tomatis_flac_enc_t enc, uint8_t** out, int64_t* out_len);
+/* Streaming to a file: take (and drop) the frame bytes encoded so far (free
+ * with tomatis_flac_free); at the end write the 42-byte header from
+ * tomatis_flac_enc_header over a 42-byte placeholder at offset 0. */
+int tomatis_flac_enc_take(tomatis_flac_enc_t enc, uint8_t** out, int64_t* out_len);
+int tomatis_flac_enc_header(tomatis_flac_enc_t enc, uint8_t* hdr42);
 void tomatis_flac_enc_close(tomatis_flac_enc_t enc);
 
 /* Byte offset of the first audio frame (after the metadata blocks), or -1. */

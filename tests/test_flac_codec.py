@@ -358,3 +358,30 @@ def test_byte_range_decode_reassembles():
                 assert lo.value == got
                 got = hi.value
         assert got == n and np.array_equal(pcm, x)
+
+
+def test_streaming_encoder_take_and_header():
+    """take() drains the frame bytes as they are encoded; header + the drained
+    parts == the whole-buffer stream (fileio's streamed file write)."""
+    import ctypes as C
+    from tomatis_audio_processor_amd import fileio
+    h = fileio._flac()
+    rng = np.random.default_rng(10)
+    n, ch = 4096 * 9 + 5, 2
+    x = rng.integers(-(1 << 23), 1 << 23, size=(n, ch)).astype(np.int32)
+    whole = audio_io.flac_encode_int(x, 96000, 24)
+    enc = C.c_void_p()
+    assert h.tomatis_flac_enc_open(ch, 96000, 24, C.byref(enc)) == 0
+    parts = []
+    out = C.POINTER(C.c_uint8)()
+    ln = C.c_int64()
+    for a, b in ((0, 4096 * 4), (4096 * 4, 4096 * 8), (4096 * 8, n)):
+        seg = np.ascontiguousarray(x[a:b])
+        assert h.tomatis_flac_enc_push(enc, seg.ctypes.data, b - a) == 0
+        assert h.tomatis_flac_enc_take(enc, C.byref(out), C.byref(ln)) == 0
+        parts.append(C.string_at(out, ln.value))
+        h.tomatis_flac_free(out)
+    hdr = (C.c_uint8 * 42)()
+    assert h.tomatis_flac_enc_header(enc, hdr) == 0
+    h.tomatis_flac_enc_close(enc)
+    assert bytes(hdr) + b"".join(parts) == whole

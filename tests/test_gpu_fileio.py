@@ -31,7 +31,7 @@ def test_flac_read_device_matches_host(tmp_path, n, ch, sub):
                                   host.view(np.uint32))
 
 
-@pytest.mark.parametrize("n,ch", [(48000 * 5 + 3, 2), (4096 * 256 * 2 + 4096 * 3 + 17, 2),
+@pytest.mark.parametrize("n,ch", [(48000 * 5 + 3, 2), (4096 * 1024 * 2 + 4096 * 3 + 17, 2),
                                   (1000, 1)])
 def test_flac_write_device_byte_identical(tmp_path, n, ch):
     torch, audio_io, fileio = _mods()

@@ -740,6 +740,8 @@ int tomatis_flac_encode(const int32_t* pcm, int64_t frames, int32_t ch, int32_t 
 
 void tomatis_flac_free(uint8_t* p) { free(p); }
 
+int tomatis_flac_enc_finish(tomatis_flac_enc_t e, uint8_t** out, int64_t* out_len);
+
 struct tomatis_flac_enc_s {
   int ch = 0, sr = 0, bps = 0;
   int64_t frames = 0;  // pushed so far (always a multiple of kBlock until the last push)
@@ -796,6 +798,22 @@ int tomatis_flac_enc_push(tomatis_flac_enc_t e, const int32_t* pcm, int64_t fram
   return TOMATIS_FLAC_OK;
 }
 
+// the 42-byte stream header ("fLaC" + STREAMINFO) alone, for a caller that
+// wrote the frames itself (tomatis_flac_enc_take) after a 42-byte placeholder
+int tomatis_flac_enc_header(tomatis_flac_enc_t e, uint8_t* hdr42) {
+  if (!e || !hdr42) return TOMATIS_FLAC_E_ARG;
+  std::vector<uint8_t> keep;
+  keep.swap(e->body);
+  uint8_t* o = nullptr;
+  int64_t n = 0;
+  const int rc = tomatis_flac_enc_finish(e, &o, &n);
+  keep.swap(e->body);
+  if (rc) return rc;
+  memcpy(hdr42, o, 42);
+  free(o);
+  return TOMATIS_FLAC_OK;
+}
+
 int tomatis_flac_enc_finish(tomatis_flac_enc_t e, uint8_t** out, int64_t* out_len) {
   if (!e || !out || !out_len) return TOMATIS_FLAC_E_ARG;
   const int64_t frames = e->frames;
@@ -825,6 +843,19 @@ int tomatis_flac_enc_finish(tomatis_flac_enc_t e, uint8_t** out, int64_t* out_le
   if (!e->body.empty()) memcpy(o + hdr, e->body.data(), e->body.size());
   *out = o;
   *out_len = (int64_t)(hdr + e->body.size());
+  return TOMATIS_FLAC_OK;
+}
+
+int tomatis_flac_enc_take(tomatis_flac_enc_t e, uint8_t** out, int64_t* out_len) {
+  if (!e || !out || !out_len) return TOMATIS_FLAC_E_ARG;
+  *out = nullptr;
+  *out_len = (int64_t)e->body.size();
+  if (e->body.empty()) return TOMATIS_FLAC_OK;
+  uint8_t* o = (uint8_t*)malloc(e->body.size());
+  if (!o) return TOMATIS_FLAC_E_NOMEM;
+  memcpy(o, e->body.data(), e->body.size());
+  e->body.clear();
+  *out = o;
   return TOMATIS_FLAC_OK;
 }
 

@@ -9,10 +9,11 @@ ingest   FLAC bytes -> K byte ranges decoded on host threads into one
          samples are DMA'd to HBM on a copy stream while the next range
          decodes; int -> float32 (libsndfile's 2^(bps-1) rule) on the device.
 egress   float32 -> PCM_24 on the device (``tomatis_float_to_pcm``), then
-         segments of 2^20 frames D2H into two alternating page-locked
+         segments of 2^22 frames D2H into two alternating page-locked
          buffers on a copy stream, each encoded on host threads
-         (``tomatis_flac_enc_push``) while the next one is in flight; the
-         stream is byte-identical to a whole-buffer encode.
+         (``tomatis_flac_enc_push``) while the next one is in flight, and
+         written to the file by a writer thread while later segments encode;
+         the stream is byte-identical to a whole-buffer encode.
 
 WAV files (and any format when libsndfile is importable) go through
 ``audio_io`` on the host as before; the reference's FLAC -> WAV fallback on an
@@ -28,7 +29,7 @@ import numpy as np
 from . import audio_io
 from ._lib import check, lib, ptr, stream_handle
 
-SEG_FRAMES = 4096 * 256      # egress segment (a whole number of FLAC blocks)
+SEG_FRAMES = 4096 * 1024     # egress segment (a whole number of FLAC blocks)
 IN_RANGES = 8                # ingest byte ranges
 
 
@@ -48,6 +49,8 @@ def _flac():
         h.tomatis_flac_enc_finish.argtypes = [P, C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(I64)]
         h.tomatis_flac_enc_close.argtypes = [P]
         h.tomatis_flac_enc_close.restype = None
+        h.tomatis_flac_enc_take.argtypes = [P, C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(I64)]
+        h.tomatis_flac_enc_header.argtypes = [P, P]
         h.tomatis_flac_first_frame.argtypes = [P, I64]
         h.tomatis_flac_first_frame.restype = I64
         h.tomatis_flac_decode_bytes.argtypes = [P, I64, I64, I64, P, I64, C.POINTER(I64),
@@ -132,8 +135,11 @@ def _read_flac_device(path, timer=None):
     return x[:n * ch], n, ch, sr
 
 
-def encode_flac_device(y, n: int, ch: int, sr: int, bps: int = 24, timer=None) -> bytes:
-    """FLAC stream of the device float32 samples y [n*ch] at ``bps`` bits."""
+def _encode_segments(y, n, ch, sr, bps, sink, timer=None):
+    """Quantise on the device, then per segment of SEG_FRAMES frames: D2H into
+    one of two page-locked buffers on a copy stream while the host encodes the
+    previous one; every segment's frame bytes go to ``sink``.  Returns the
+    42-byte stream header (STREAMINFO)."""
     torch = _torch()
     h = _flac()
     t0 = time.perf_counter()
@@ -159,6 +165,8 @@ def encode_flac_device(y, n: int, ch: int, sr: int, bps: int = 24, timer=None) -
 
         if K:
             issue(0)
+        out = C.POINTER(C.c_uint8)()
+        ln = C.c_int64()
         for k in range(K):
             if k + 1 < K:
                 issue(k + 1)          # its buffer's previous segment was pushed at k - 1
@@ -166,31 +174,65 @@ def encode_flac_device(y, n: int, ch: int, sr: int, bps: int = 24, timer=None) -
             a, b = k * seg, min(n, (k + 1) * seg)
             _err(h.tomatis_flac_enc_push(enc, pins[k % 2].data_ptr(), b - a),
                  "FLAC encode failed")
-        out = C.POINTER(C.c_uint8)()
-        ln = C.c_int64()
-        _err(h.tomatis_flac_enc_finish(enc, C.byref(out), C.byref(ln)), "FLAC encode failed")
-        try:
-            blob = C.string_at(out, ln.value)
-        finally:
-            h.tomatis_flac_free(out)
+            _err(h.tomatis_flac_enc_take(enc, C.byref(out), C.byref(ln)), "FLAC encode failed")
+            if ln.value:
+                try:
+                    sink(C.string_at(out, ln.value))
+                finally:
+                    h.tomatis_flac_free(out)
+        hdr = (C.c_uint8 * 42)()
+        _err(h.tomatis_flac_enc_header(enc, hdr), "FLAC encode failed")
     finally:
         h.tomatis_flac_enc_close(enc)
     if timer is not None:
         timer.add("d2h+encode", t0)
-    return blob
+    return bytes(hdr)
+
+
+def encode_flac_device(y, n: int, ch: int, sr: int, bps: int = 24, timer=None) -> bytes:
+    """FLAC stream of the device float32 samples y [n*ch] at ``bps`` bits."""
+    parts = []
+    hdr = _encode_segments(y, n, ch, sr, bps, parts.append, timer)
+    return hdr + b"".join(parts)
 
 
 def write_device(out_path: str, y, n: int, ch: int, sr: int, log=print, timer=None):
     """FLAC PCM_24 of device samples y [n*ch], else the reference's WAV fallback
     at ``out_path.replace('.flac', '.wav')`` (src/process_tomatis.py:242-251).
-    Returns (written_path, is_flac)."""
+    Frame bytes are written by a writer thread while later segments encode;
+    the header goes over a placeholder at the end.  Returns (written_path, is_flac)."""
     if audio_io.have_soundfile():
         return audio_io.write_with_fallback(out_path, y.cpu().numpy().reshape(n, ch), sr, log=log)
+    import queue
+    import threading
     try:
-        blob = encode_flac_device(y, n, ch, sr, 24, timer)
-        t0 = time.perf_counter()
         with open(out_path, "wb") as f:
-            f.write(blob)
+            f.write(b"\0" * 42)
+            q = queue.Queue(maxsize=4)
+            err = []
+
+            def writer():
+                while True:
+                    b = q.get()
+                    if b is None:
+                        return
+                    try:
+                        f.write(b)
+                    except Exception as e:  # reported after the encode
+                        err.append(e)
+
+            th = threading.Thread(target=writer, daemon=True)
+            th.start()
+            try:
+                hdr = _encode_segments(y, n, ch, sr, 24, q.put, timer)
+            finally:
+                q.put(None)
+                th.join()
+            if err:
+                raise err[0]
+            t0 = time.perf_counter()
+            f.seek(0)
+            f.write(hdr)
         if timer is not None:
             timer.add("write", t0)
         log("[OK] 输出格式: FLAC 24-bit")
