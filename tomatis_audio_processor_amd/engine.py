@@ -144,6 +144,23 @@ def _host_pool():
     return _POOL
 
 
+def _levels_threaded(r: np.ndarray, out: np.ndarray):
+    """``dsp.r_to_level(r)`` into ``out`` in slices on the host pool (numpy's
+    elementwise log10 releases the GIL; slicing does not change any value)."""
+    n = len(r)
+    if n < (1 << 16):
+        out[:] = dsp.r_to_level(r)
+        return
+    k = 16
+    edges = np.linspace(0, n, k + 1).astype(np.int64)
+
+    def part(i):
+        a, b = edges[i], edges[i + 1]
+        out[a:b] = dsp.r_to_level(r[a:b])
+
+    list(_host_pool().map(part, range(k)))
+
+
 def _set_gate(st: TomatisStream, Ton: float, Toff: float):
     on, oe, off, fe = dsp.gate_bits(Ton, Toff)
     st.on_bits, st.off_bits = on, off
@@ -443,6 +460,7 @@ class AdaptivePipeline:
         self.t_out = torch.empty(max(1, ss.n_streams), dtype=torch.float64, device=dev)
         self.peaks = torch.zeros(max(1, self.plan.total_chunks), dtype=torch.int32, device=dev)
         self.inpk = torch.zeros(max(1, ss.n_streams), dtype=torch.int32, device=dev)
+        self._lv_pin = None   # page-locked staging of the host levels (allocated once)
         self.gains = torch.from_numpy(np.stack(rows)).to(dev)
         self.n_rows = len(rows)
         self.out_offs = out_offs
@@ -474,22 +492,27 @@ class AdaptivePipeline:
             check(L.tomatis_levels(P, ptr(ss.x), ptr(self.r32), F32, hs), "levels f32")
         if F64 in prec:
             check(L.tomatis_levels(P, ptr(ss.x), ptr(self.r64), F64, hs), "levels f64")
-        r32 = self.r32.cpu().numpy() if F32 in prec else None
-        r64 = self.r64.cpu().numpy() if F64 in prec else None
-        # levels of every frame in one elementwise call per precision (identical
-        # to the reference's per-frame calls), then per-stream statistics
-        lv32 = dsp.r_to_level(r32) if r32 is not None else None
-        lv64 = dsp.r_to_level(r64) if r64 is not None else None
-        if lv64 is None:
-            lv = lv32
-        elif lv32 is None:
-            lv = lv64
+        Ft = self.plan.total_frames
+        r32 = self.r32.cpu().numpy()[:Ft] if F32 in prec else None
+        r64 = self.r64.cpu().numpy()[:Ft] if F64 in prec else None
+        # levels of every frame by the same elementwise numpy call as the
+        # reference's per-frame one (threaded slices), straight into the
+        # page-locked staging block of the upload; then per-stream statistics
+        if self._lv_pin is None:
+            self._lv_pin = torch.empty(max(1, Ft), dtype=torch.float64, pin_memory=True)
+        lv = self._lv_pin.numpy()[:Ft]
+        if r64 is None:
+            _levels_threaded(r32, lv)
+        elif r32 is None:
+            _levels_threaded(r64, lv)
         else:
-            lv = np.empty(self.plan.total_frames, np.float64)
+            lv32 = np.empty(Ft, np.float64)
+            lv64 = np.empty(Ft, np.float64)
+            _levels_threaded(r32, lv32)
+            _levels_threaded(r64, lv64)
             for i in range(ss.n_streams):
                 a, F = sts[i].frame_base, sts[i].n_frames
                 lv[a:a + F] = (lv32 if prec[i] == F32 else lv64)[a:a + F]
-        lv = np.ascontiguousarray(lv[:self.plan.total_frames], np.float64)
         tlh = np.empty((ss.n_streams, 3), np.float64)
 
         def stream_stats(i):  # numpy releases the GIL in partition
@@ -505,23 +528,23 @@ class AdaptivePipeline:
             list(_host_pool().map(stream_stats, range(ss.n_streams)))
         else:
             stream_stats(0)
-        self.levels.copy_(torch.from_numpy(lv))
+        self.levels[:Ft].copy_(self._lv_pin[:Ft], non_blocking=True)
         tl = torch.from_numpy(tlh.reshape(-1)).to(self.levels.device)
         self._tlh = tl
         # 3. bisection + min-hold states + alpha + rows
         check(L.tomatis_minhold_bisect(P, ptr(self.levels), ptr(tl), self.target_c2,
                                        self.hyst_db, ptr(self.t_out), ptr(self.states),
                                        ptr(self.rows), ptr(self.alpha), hs), "minhold_bisect")
-        # 4. STFT-gain-OLA, normalise max(w,1e-8), restore, global limiter
+        # 4. STFT-gain-OLA, normalise max(w,1e-8), restore, global limiter (one
+        #    chunk per stream: fused into the transform when its runs allow)
         self.peaks.zero_()
         if marks:
             marks[0].record()
-        check(L.tomatis_stft_ola(P, ptr(ss.x), ptr(self.gains), self.n_rows, ptr(self.rows),
-                                 ptr(self.y), ptr(self.peaks), hs), "stft_ola")
+        check(L.tomatis_stft_ola_limited(P, ptr(ss.x), ptr(self.gains), self.n_rows,
+                                         ptr(self.rows), ptr(self.y), ptr(self.peaks),
+                                         PEAK_LIMIT, hs), "stft_ola_limited")
         if marks:
             marks[1].record()
-        check(L.tomatis_apply_limiter(P, ptr(self.y), ptr(self.peaks), PEAK_LIMIT, hs),
-              "apply_limiter")
         self.prec = prec
         return self.result()
 
