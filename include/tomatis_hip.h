@@ -178,6 +178,14 @@ int tomatis_gate_segment_sums(tomatis_plan_t plan, const float* r, int32_t* sums
 int tomatis_gate_std_carry(tomatis_plan_t plan, const float* r, const int32_t* carry_host,
                            uint8_t* states, uint16_t* rows, void* hip_stream);
 
+/* Adaptive: per stream, t_lo_hi_med[3*s..3*s+2] = (np.percentile(v, 5),
+ * np.percentile(v, 95), np.median(v)) of v = the stream's levels > -70, or
+ * (NaN, NaN, np.median(levels)) when none is valid, (NaN, NaN, 0) for a stream
+ * without frames -- bit-identical to numpy (exact selection + numpy's linear
+ * interpolation).  Replaces src/process_tomatis_adaptive.py:123-131. */
+int tomatis_level_stats(tomatis_plan_t plan, const double* levels, double* t_lo_hi_med,
+                        void* hip_stream);
+
 /* Adaptive: bisection for the min-hold threshold per stream
  * (find_optimal_threshold), final states, alpha and gain rows (2+m).
  * levels: f64 per frame; t_lo_hi_med: 3 doubles per stream (p5, p95, median of

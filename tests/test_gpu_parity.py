@@ -287,3 +287,33 @@ def test_adaptive_alpha_long_streams(xfade_ms):
         a, F = res.frame_base[i], res.n_frames[i]
         rows = pipe.rows[a:a + F].cpu().numpy().astype(np.int64)
         assert np.array_equal(rows, 2 + np.rint(ref * max(pipe.xf, 1)).astype(np.int64))
+
+
+@pytest.mark.parametrize("min_hold_ms,hop,secs", [(0.0, 512, 40), (250.0, 512, 770),
+                                                  (3000.0, 128, 150)])
+def test_minhold_bisect_table_paths(min_hold_ms, hop, secs):
+    """k_minhold (per-threshold 2-bit symbols, segment transfer tables) against the
+    reference automaton and bisection (process_tomatis_adaptive.py:87-154) on the
+    GPU's own levels: min-hold 0; a stream of > 65536 frames (symbols outside
+    LDS); a 1034-frame min-hold (transfer tables outside LDS)."""
+    torch, E = _engine()
+    from oracle import tomatis_oracle as orc
+    sr, rng = 44100, np.random.default_rng(secs)
+    n = sr * secs
+    steps = np.repeat(10 ** (rng.uniform(-75, -5, n // 5000 + 1) / 20), 5000)[:n]
+    x = (rng.standard_normal((n, 2)) * steps[:, None] * 0.3).astype(np.float32)
+    ss = E.StreamSet.from_arrays([x, x[: n // 3]], sr)
+    pipe = E.AdaptivePipeline(ss, n_fft=2048, hop=hop, min_hold_ms=min_hold_ms)
+    res = pipe.run()
+    torch.cuda.synchronize()
+    lv_all = res.extra["levels"].cpu().numpy()
+    T_all = res.extra["thresholds"].cpu().numpy()
+    for i in range(2):
+        a, F = res.frame_base[i], res.n_frames[i]
+        lv = lv_all[a:a + F]
+        T = orc.optimal_threshold(lv, lv > -70, 3.0, pipe.mh, 0.5)
+        assert T_all[i] == T, (i, T_all[i], T)
+        st = res.stream_states(i)
+        ref = orc.gate_minhold(lv, T, 3.0, pipe.mh)
+        assert 0 < np.count_nonzero(ref == 2) < F
+        np.testing.assert_array_equal(st, ref)

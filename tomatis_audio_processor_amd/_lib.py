@@ -78,6 +78,7 @@ _SIGS = {
     "tomatis_plan_gate_segments": (C.c_int32, [_P]),
     "tomatis_gate_segment_sums": (C.c_int, [_P, _P, _P, _P]),
     "tomatis_gate_std_carry": (C.c_int, [_P, _P, _P, _P, _P, _P]),
+    "tomatis_level_stats": (C.c_int, [_P, _P, _P, _P]),
     "tomatis_minhold_bisect": (C.c_int, [_P, _P, _P, C.c_double, C.c_double, _P, _P, _P,
                                          _P, _P]),
     "tomatis_stft_ola": (C.c_int, [_P, _P, _P, C.c_int32, _P, _P, _P, _P]),

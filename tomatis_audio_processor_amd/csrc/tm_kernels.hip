@@ -31,7 +31,6 @@ using namespace tshared;
 namespace {
 
 constexpr int kSeg = 1024;           // gate segment length (frames)
-constexpr int kMhSeg = 256;          // min-hold segment length (frames)
 constexpr int kLevelLds = 12288;     // floats of LDS for the levels span
 constexpr int kMaxGateStates = 1024;
 
@@ -638,37 +637,211 @@ __global__ void k_alpha_xfade(const TomatisStream* __restrict__ st, int n_stream
 // state id = (C - 1) * (mh + 1) + min(since, mh)
 // ===========================================================================
 constexpr int kMhAlphaChunks = 2048;  // alpha chunks per stream (LDS carries)
-__device__ __forceinline__ int mh_step(int id, double lv, double ton, double toff, int mh) {
-  const int c2 = id / (mh + 1);
-  int since = id - c2 * (mh + 1);
-  since = min(since + 1, mh);
-  if (since >= mh) {
-    if (!c2) {
-      if (lv >= ton) return (mh + 1) * 1 + 0;
-    } else {
-      if (lv <= toff) return 0;
-    }
-  }
-  return c2 * (mh + 1) + since;
+constexpr int kMhLdsTf = 8192;        // (segment, start state) transfer entries held in LDS
+constexpr int kMhLdsSym = 4096;       // symbol words held in LDS (65536 frames)
+
+// Segment length (frames, a multiple of 16 = one symbol word): at least 256,
+// few enough segments that the (segment, start) transfer table fits in LDS and
+// the final pass's segment starts fit its 4096-entry table.  Host and device.
+__host__ __device__ inline int64_t mh_seg_len(int64_t F, int ns) {
+  int64_t seg = 256;
+  const int64_t a = (F * ns + kMhLdsTf - 1) / kMhLdsTf, b = (F + 4095) / 4096;
+  seg = a > seg ? a : seg;
+  seg = b > seg ? b : seg;
+  return (seg + 15) & ~(int64_t)15;
 }
 
-// workspace per stream: tf/cnt per (segment, state)
-__device__ void mh_simulate(const double* __restrict__ lv, int64_t F, double ton, double toff,
-                            int mh, uint16_t* __restrict__ tf, int32_t* __restrict__ cnt) {
+// Per bisection threshold the levels reduce to 2-bit symbols per frame
+// (bit 0: level >= t_on, bit 1: level <= t_off; NaN sets neither), 16 frames
+// per u32 word; the min-hold walk then only needs the symbols.
+__device__ void mh_symbols(const double* __restrict__ lv, int64_t F, double ton, double toff,
+                           uint32_t* __restrict__ sym) {
+  const int64_t nw = (F + 15) >> 4;
+  for (int64_t w = threadIdx.x; w < nw; w += blockDim.x) {
+    const int64_t k0 = w << 4;
+    const int n = (int)min<int64_t>(16, F - k0);
+    uint32_t b = 0;
+    for (int j = 0; j < n; ++j) {
+      const double l = lv[k0 + j];
+      b |= (l >= ton ? 1u : 0u) << (2 * j);
+      b |= (l <= toff ? 1u : 0u) << (2 * j + 1);
+    }
+    sym[w] = b;
+  }
+}
+
+// state (c2, since): since = min(since + 1, mh); once saturated a C1 frame with
+// symbol bit 0 switches to (C2, 0), a C2 frame with bit 1 to (C1, 0)
+// (src/process_tomatis_adaptive.py:87-120, simulate_gate with min_hold).
+// State id = c2 * (mh + 1) + since.
+struct MhState {
+  int c2, since;
+};
+__device__ __forceinline__ void mh_word(MhState& st, uint32_t w, int n, int mh, int& c) {
+  for (int j = 0; j < n; ++j) {
+    st.since = min(st.since + 1, mh);
+    const int sw = (st.since == mh) & (int)((w >> (2 * j + st.c2)) & 1u);
+    st.c2 ^= sw;
+    st.since = sw ? 0 : st.since;
+    c += st.c2;
+  }
+}
+
+// transfer table of every (segment, start state): end state and C2 frames
+__device__ void mh_simulate(const uint32_t* sym, int64_t F, int64_t seg, int mh,
+                            uint16_t* tf, int32_t* cnt) {
   const int ns = 2 * (mh + 1);
-  const int nseg = (int)((F + kMhSeg - 1) / kMhSeg);
+  const int nseg = (int)((F + seg - 1) / seg);
   const int nwork = nseg * ns;
   for (int w = threadIdx.x; w < nwork; w += blockDim.x) {
     const int sg = w / ns, s0 = w - sg * ns;
-    const int64_t k0 = (int64_t)sg * kMhSeg;
-    const int nf = (int)min<int64_t>(kMhSeg, F - k0);
-    int id = s0, c = 0;
-    for (int i = 0; i < nf; ++i) {
-      id = mh_step(id, lv[k0 + i], ton, toff, mh);
-      c += (id > mh) ? 1 : 0;
-    }
-    tf[w] = (uint16_t)id;
+    const int64_t k0 = (int64_t)sg * seg;
+    const int64_t k1 = min<int64_t>(k0 + seg, F);
+    MhState st{s0 > mh ? 1 : 0, s0 > mh ? s0 - (mh + 1) : s0};
+    int c = 0;
+    for (int64_t k = k0; k < k1; k += 16)
+      mh_word(st, sym[k >> 4], (int)min<int64_t>(16, k1 - k), mh, c);
+    tf[w] = (uint16_t)(st.c2 * (mh + 1) + st.since);
     cnt[w] = c;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// adaptive: per-stream order statistics of the valid levels
+// (src/process_tomatis_adaptive.py:123-131: valid = levels > -70;
+//  np.percentile(valid, 5), np.percentile(valid, 95), np.median(valid); with no
+//  valid level the threshold is np.median(levels)).  Exact selection by an
+//  8-bit radix walk over order-preserving u64 keys of the f64 levels, for up
+//  to six ranks at once (the two neighbours of each percentile position and
+//  the one or two middle ranks); the numpy 'linear' interpolation and median
+//  rule are then evaluated in the same IEEE operations as numpy (no
+//  contraction), so t_lo_hi_med is bit-identical to the host statistics.
+// ---------------------------------------------------------------------------
+constexpr double kValidLevel = -70.0;
+constexpr int kSelRanks = 6;
+
+__device__ __forceinline__ uint64_t f64_key(double v) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double key_f64(uint64_t k) {
+  const uint64_t u = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
+  return __longlong_as_double((long long)u);
+}
+
+__global__ __launch_bounds__(1024) void k_level_stats(const double* __restrict__ levels,
+                                                      const TomatisStream* __restrict__ st,
+                                                      double* __restrict__ tlh) {
+#pragma clang fp contract(off)
+  const int s = blockIdx.x;
+  const int64_t F = st[s].n_frames;
+  const double* lv = levels + st[s].frame_base;
+  __shared__ uint32_t hist[kSelRanks][256];
+  __shared__ uint64_t pre[kSelRanks];
+  __shared__ int64_t want[kSelRanks];
+  __shared__ unsigned long long sh_cnt;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) sh_cnt = 0;
+  __syncthreads();
+  unsigned long long c = 0;
+  for (int64_t i = tid; i < F; i += blockDim.x) c += (lv[i] > kValidLevel) ? 1 : 0;
+  for (int o = 32; o; o >>= 1) c += __shfl_xor(c, o);
+  if (lane == 0) atomicAdd(&sh_cnt, c);
+  __syncthreads();
+  const int64_t nv = (int64_t)sh_cnt;
+  const bool all = (nv == 0);   // no valid level: median over every level
+  const int64_t n = all ? F : nv;
+  if (n == 0) {
+    if (tid == 0) {
+      tlh[3 * s + 0] = __longlong_as_double(0x7ff8000000000000ll);
+      tlh[3 * s + 1] = __longlong_as_double(0x7ff8000000000000ll);
+      tlh[3 * s + 2] = 0.0;
+    }
+    return;
+  }
+  // ranks (numpy 2.x _quantile 'linear': virtual index (n-1)*q)
+  const double q[2] = {5.0 / 100.0, 95.0 / 100.0};
+  int64_t pi[2], ni[2];
+  double gam[2];
+  for (int j = 0; j < 2; ++j) {
+    const double vi = (double)(n - 1) * q[j];
+    const double prev = floor(vi);
+    const bool above = vi >= (double)(n - 1);
+    pi[j] = above ? n - 1 : (int64_t)prev;
+    ni[j] = above ? n - 1 : (int64_t)prev + 1;
+    gam[j] = above ? 0.0 : vi - prev;
+  }
+  const int64_t h = n / 2;
+  if (tid == 0) {
+    want[0] = pi[0]; want[1] = ni[0]; want[2] = pi[1]; want[3] = ni[1];
+    want[4] = (n % 2 == 0) ? h - 1 : h;
+    want[5] = h;
+    for (int r = 0; r < kSelRanks; ++r) pre[r] = 0;
+  }
+  __syncthreads();
+  for (int pass = 0; pass < 8; ++pass) {
+    const int shift = 56 - 8 * pass;
+    const uint64_t hmask = pass ? (~0ull << (shift + 8)) : 0ull;
+    for (int i = tid; i < kSelRanks * 256; i += blockDim.x) (&hist[0][0])[i] = 0;
+    __syncthreads();
+    uint64_t pr[kSelRanks];
+    for (int r = 0; r < kSelRanks; ++r) pr[r] = pre[r];
+    for (int64_t i = tid; i < F; i += blockDim.x) {
+      const double v = lv[i];
+      if (!all && !(v > kValidLevel)) continue;
+      const uint64_t k = f64_key(v);
+      const uint32_t d = (uint32_t)(k >> shift) & 255u;
+#pragma unroll
+      for (int r = 0; r < kSelRanks; ++r)
+        if ((k & hmask) == pr[r]) atomicAdd(&hist[r][d], 1u);
+    }
+    __syncthreads();
+    if (wv < kSelRanks) {   // wave r resolves rank r's digit
+      const int r = wv;
+      const uint32_t b0 = hist[r][4 * lane], b1 = hist[r][4 * lane + 1],
+                     b2 = hist[r][4 * lane + 2], b3 = hist[r][4 * lane + 3];
+      const uint32_t tot = b0 + b1 + b2 + b3;
+      uint32_t incl = tot;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o);
+        if (lane >= o) incl += t;
+      }
+      const int64_t k = want[r];   // rank within the remaining prefix class
+      const int64_t ex = (int64_t)(incl - tot);
+      if (k >= ex && k < (int64_t)incl) {
+        int64_t acc = ex;
+        int dsel = 4 * lane;
+        const uint32_t bb[4] = {b0, b1, b2, b3};
+        for (int j = 0; j < 4; ++j) {
+          if (k < acc + (int64_t)bb[j]) { dsel = 4 * lane + j; break; }
+          acc += bb[j];
+        }
+        want[r] = k - acc;
+        pre[r] = pre[r] | ((uint64_t)dsel << shift);
+      }
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    double val[kSelRanks];
+    for (int r = 0; r < kSelRanks; ++r) val[r] = key_f64(pre[r]);
+    double med;
+    if (n % 2) med = val[5] + 0.0;
+    else med = ((0.0 + val[4]) + val[5]) / 2.0;
+    if (all) {
+      tlh[3 * s + 0] = __longlong_as_double(0x7ff8000000000000ll);
+      tlh[3 * s + 1] = __longlong_as_double(0x7ff8000000000000ll);
+      tlh[3 * s + 2] = med;
+      return;
+    }
+    for (int j = 0; j < 2; ++j) {
+      const double a = val[2 * j], b = val[2 * j + 1];
+      const double d = b - a;
+      double lerp = a + d * gam[j];
+      if (gam[j] >= 0.5) lerp = b - d * (1.0 - gam[j]);
+      tlh[3 * s + j] = lerp;
+    }
+    tlh[3 * s + 2] = med;
   }
 }
 
@@ -679,6 +852,8 @@ __global__ __launch_bounds__(1024) void k_minhold(const double* __restrict__ lev
                                                   int alpha_adaptive, uint16_t* __restrict__ ws_tf,
                                                   int32_t* __restrict__ ws_cnt,
                                                   const int64_t* __restrict__ ws_off,
+                                                  uint32_t* __restrict__ ws_sym,
+                                                  const int64_t* __restrict__ ws_soff,
                                                   double* __restrict__ t_out,
                                                   uint8_t* __restrict__ states,
                                                   uint16_t* __restrict__ rows,
@@ -687,13 +862,19 @@ __global__ __launch_bounds__(1024) void k_minhold(const double* __restrict__ lev
   const TomatisStream S = st[s];
   const int64_t F = S.n_frames;
   const double* lv = levels + S.frame_base;
-  uint16_t* tf = ws_tf + ws_off[s];
-  int32_t* cnt = ws_cnt + ws_off[s];
   const int ns = 2 * (mh + 1);
-  const int nseg = (int)((F + kMhSeg - 1) / kMhSeg);
+  const int64_t seg = mh_seg_len(F, ns);
+  const int nseg = (int)((F + seg - 1) / seg);
   const int init_id = mh;  // C1, since = mh
+  __shared__ uint16_t tf_l[kMhLdsTf];
+  __shared__ int32_t cnt_l[kMhLdsTf];
+  __shared__ uint32_t sym_l[kMhLdsSym];
+  const bool tf_lds = (int64_t)nseg * ns <= kMhLdsTf;
+  uint16_t* tf = tf_lds ? tf_l : ws_tf + ws_off[s];
+  int32_t* cnt = tf_lds ? cnt_l : ws_cnt + ws_off[s];
+  const int64_t nw = (F + 15) >> 4;
+  uint32_t* sym = nw <= kMhLdsSym ? sym_l : ws_sym + ws_soff[s];
   __shared__ double sh_T;
-  __shared__ int sh_done;
   __shared__ int sh_count;
   double t_low = tlh[3 * s + 0], t_high = tlh[3 * s + 1];
   double best_T = tlh[3 * s + 2], best_diff = 1.0;
@@ -702,8 +883,9 @@ __global__ __launch_bounds__(1024) void k_minhold(const double* __restrict__ lev
     for (int it = 0; it < 30; ++it) {
       const double t_mid = (t_low + t_high) / 2;
       const double ton = t_mid + hyst / 2, toff = t_mid - hyst / 2;
-      mh_simulate(lv, F, ton, toff, mh, tf, cnt);
-      __threadfence_block();
+      mh_symbols(lv, F, ton, toff, sym);
+      __syncthreads();
+      mh_simulate(sym, F, seg, mh, tf, cnt);
       __syncthreads();
       if (threadIdx.x == 0) {
         int id = init_id, c = 0;
@@ -723,7 +905,6 @@ __global__ __launch_bounds__(1024) void k_minhold(const double* __restrict__ lev
       if (diff < 0.01) break;
       if (c2 < target) t_high = t_mid;
       else t_low = t_mid;
-      __syncthreads();
     }
   }
   if (threadIdx.x == 0) {
@@ -733,25 +914,34 @@ __global__ __launch_bounds__(1024) void k_minhold(const double* __restrict__ lev
   __syncthreads();
   const double T = sh_T;
   const double ton = T + hyst / 2, toff = T - hyst / 2;
-  // final states: sequential per segment starts, then parallel per segment
-  mh_simulate(lv, F, ton, toff, mh, tf, cnt);
+  // final states: segment transfer tables, sequential segment starts, then
+  // every segment re-walked from its start writing states
+  mh_symbols(lv, F, ton, toff, sym);
+  __syncthreads();
+  mh_simulate(sym, F, seg, mh, tf, cnt);
   __syncthreads();
   __shared__ uint16_t seg_start[4096];
   if (threadIdx.x == 0) {
     int id = init_id;
     for (int g = 0; g < nseg; ++g) {
-      if (g < 4096) seg_start[g] = (uint16_t)id;
+      seg_start[g] = (uint16_t)id;
       id = tf[(int64_t)g * ns + id];
     }
   }
   __syncthreads();
   for (int g = threadIdx.x; g < nseg; g += blockDim.x) {
-    int id = (g < 4096) ? seg_start[g] : init_id;
-    const int64_t k0 = (int64_t)g * kMhSeg;
-    const int nf = (int)min<int64_t>(kMhSeg, F - k0);
-    for (int i = 0; i < nf; ++i) {
-      id = mh_step(id, lv[k0 + i], ton, toff, mh);
-      states[S.frame_base + k0 + i] = (id > mh) ? 2 : 1;
+    const int id0 = seg_start[g];
+    MhState stt{id0 > mh ? 1 : 0, id0 > mh ? id0 - (mh + 1) : id0};
+    const int64_t k0 = (int64_t)g * seg;
+    const int64_t k1 = min<int64_t>(k0 + seg, F);
+    for (int64_t k = k0; k < k1; k += 16) {
+      const uint32_t w = sym[k >> 4];
+      const int n = (int)min<int64_t>(16, k1 - k);
+      for (int j = 0; j < n; ++j) {
+        int c = 0;
+        mh_word(stt, w >> (2 * j), 1, mh, c);
+        states[S.frame_base + k + j] = stt.c2 ? 2 : 1;
+      }
     }
   }
   __syncthreads();
@@ -1020,6 +1210,8 @@ struct tomatis_plan_s {
   uint16_t* mh_tf = nullptr;
   int32_t* mh_cnt = nullptr;
   int64_t* mh_off = nullptr;
+  uint32_t* mh_sym = nullptr;
+  int64_t* mh_soff = nullptr;
   float* gperm = nullptr;
   int gperm_rows = 0;
   // fused limiter
@@ -1095,7 +1287,7 @@ int tomatis_plan_destroy(tomatis_plan_t p) {
   if (!p) return TOMATIS_OK;
   void* ptrs[] = {p->st, p->runs, p->lblocks, p->segs, p->seg_first, p->seg_count, p->tf,
                   p->seg_start, p->win, p->win2, p->winv, p->twN, p->twP, p->scratch,
-                  p->pos_base, p->chunks, p->mh_tf, p->mh_cnt, p->mh_off, p->gperm,
+                  p->pos_base, p->chunks, p->mh_tf, p->mh_cnt, p->mh_off, p->mh_sym, p->mh_soff, p->gperm,
                   p->grp_base, p->leaf_base, p->leaves, p->gsum, p->gcarry, p->gcarry_in,
                   p->aq, p->afin, p->acin,
                   p->chunk_need, p->chunk_done, p->chunk_rng, p->err, p->twL};
@@ -1423,19 +1615,25 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
     if (hipMalloc(reinterpret_cast<void**>(&p->scratch), (size_t)p->total_frames * N * per))
       return TOMATIS_E_NOMEM;
   }
-  // --- min-hold workspace ---
+  // --- min-hold workspace (used when a stream's tables exceed the kernel's LDS) ---
   if (d.min_hold_frames >= 0) {
     const int nsm = 2 * (d.min_hold_frames + 1);
-    std::vector<int64_t> off(ns + 1, 0);
+    std::vector<int64_t> off(ns + 1, 0), soff(ns + 1, 0);
     for (int s = 0; s < ns; ++s) {
-      const int64_t nseg = (p->hs[s].n_frames + kMhSeg - 1) / kMhSeg;
-      off[s + 1] = off[s] + nseg * nsm;
+      const int64_t F = p->hs[s].n_frames;
+      const int64_t nseg = (F + mh_seg_len(F, nsm) - 1) / mh_seg_len(F, nsm);
+      off[s + 1] = off[s] + (nseg * nsm > kMhLdsTf ? nseg * nsm : 0);
+      soff[s + 1] = soff[s] + (((F + 15) >> 4) > kMhLdsSym ? (F + 15) >> 4 : 0);
     }
     if ((rc = dalloc_copy(&p->mh_off, off))) return rc;
+    if ((rc = dalloc_copy(&p->mh_soff, soff))) return rc;
     if (off[ns] > 0) {
       if (hipMalloc(reinterpret_cast<void**>(&p->mh_tf), off[ns] * sizeof(uint16_t))) return TOMATIS_E_NOMEM;
       if (hipMalloc(reinterpret_cast<void**>(&p->mh_cnt), off[ns] * sizeof(int32_t))) return TOMATIS_E_NOMEM;
     }
+    if (soff[ns] > 0 &&
+        hipMalloc(reinterpret_cast<void**>(&p->mh_sym), soff[ns] * sizeof(uint32_t)))
+      return TOMATIS_E_NOMEM;
   }
   return TOMATIS_OK;
 }
@@ -1686,6 +1884,14 @@ int tomatis_gate_std_carry(tomatis_plan_t p, const float* r, const int32_t* carr
   return hipfail(hipStreamSynchronize(s));  // carry_host may be reused by the caller
 }
 
+int tomatis_level_stats(tomatis_plan_t p, const double* levels, double* tlh, void* hs) {
+  if (!p || !levels || !tlh) return TOMATIS_E_ARG;
+  if (p->n_streams == 0) return TOMATIS_OK;
+  hipLaunchKernelGGL(k_level_stats, dim3(p->n_streams), dim3(1024), 0, (hipStream_t)hs, levels,
+                     p->st, tlh);
+  return launch_check();
+}
+
 int tomatis_minhold_bisect(tomatis_plan_t p, const double* levels, const double* tlh,
                            double target_c2, double hyst_db, double* t_out, uint8_t* states,
                            uint16_t* rows, double* alpha_out, void* hs) {
@@ -1694,7 +1900,7 @@ int tomatis_minhold_bisect(tomatis_plan_t p, const double* levels, const double*
   hipStream_t s = (hipStream_t)hs;
   hipLaunchKernelGGL(k_minhold, dim3(p->n_streams), dim3(1024), 0, s, levels, p->st, tlh,
                      target_c2, hyst_db, p->d.min_hold_frames, p->d.xfade_frames, 1, p->mh_tf,
-                     p->mh_cnt, p->mh_off, t_out, states, rows, alpha_out);
+                     p->mh_cnt, p->mh_off, p->mh_sym, p->mh_soff, t_out, states, rows, alpha_out);
   return launch_check();
 }
 
@@ -1765,6 +1971,19 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
   A.rmax = p->generic ? 1 : p->rmax;
   A.inv_n = 1.0f / (float)N;
   A.n_rows_lds = (n_rows <= 2 && N <= 2048) ? n_rows : 0;
+  A.lds_mixed = 0;
+  A.lds_row[0] = 0;
+  A.lds_row[1] = 1;
+  if (n_rows > 2 && N <= 2048 && p->d.alpha_mode != 0 && env_int("TOMATIS_GAIN_LDS", 1) != 0) {
+    // cross-fade tables: the pure rows (alpha 0 and 1) carry most frames
+    // (xfade: rows 0/1; adaptive: rows 2 and 2 + xfade_frames = n_rows - 1)
+    A.n_rows_lds = 2;
+    A.lds_mixed = 1;
+    if (p->d.alpha_mode == 2) {
+      A.lds_row[0] = 2;
+      A.lds_row[1] = n_rows - 1;
+    }
+  }
   A.limit = limit;
   A.chunk_done = p->chunk_done;
   A.chunk_need = p->chunk_need;

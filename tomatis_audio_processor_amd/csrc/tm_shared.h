@@ -43,6 +43,8 @@ struct MainArgs {
   const float* winv;    // [hop] 1/(interior wsum) (already normalisation-rule applied)
   cf* scratch;          // generic path: [frames][N]
   int n_runs, hop, n_bins, ch, norm_mode, rmax, n_rows_lds;
+  int lds_row[2];       // GM 2: the rows held in LDS (others read from global)
+  int lds_mixed;        // 1: n_rows > 2, only lds_row[] in LDS
   float inv_n;
   // fused limiter (limit > 0): per-chunk flush counters, flushes expected,
   // output ranges; every wave rescales its own output once its chunks are final

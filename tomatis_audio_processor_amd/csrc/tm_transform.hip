@@ -175,8 +175,10 @@ typedef __attribute__((address_space(4))) const uint32_t cu32;
 // one stream and emits the hop block of every frame >= ka.  Lane L register i
 // holds stream position s_k + L + P*i; the OLA accumulator for the next frame
 // is this frame's registers shifted by SH = hop/P.
-// GLDS: the (<= 2) gain rows live in LDS in the per-lane layout.
-template <int P, int NR, int SH, int CH, bool GLDS, bool PF, bool NT, int WG>
+// GM: where the gain rows live (per-lane layout).  0: global (L2) only;
+// 1: all (<= 2) rows in LDS; 2: the two pure rows A.lds_row[0..1] in LDS, the
+// cross-fade lattice rows from global (row is wave-uniform, so is the branch).
+template <int P, int NR, int SH, int CH, int GM, bool PF, bool NT, int WG>
 __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(MainArgs A) {
 #ifdef TM_PROFILE
   const unsigned long long t_k0 = __builtin_amdgcn_s_memtime();
@@ -194,7 +196,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   __shared__ __attribute__((aligned(16))) float s_win[N];      // lane-quad layout
   __shared__ __attribute__((aligned(16))) float s_winv[SHQ * P];  // lane-quad layout
   __shared__ cf s_buf[NSEQ][G::BUF];
-  __shared__ __attribute__((aligned(16))) float s_gain[GLDS ? 2 * N : 4];
+  __shared__ __attribute__((aligned(16))) float s_gain[GM ? 2 * N : 4];
   for (int i = threadIdx.x; i < NR * P; i += WG) s_twN[i] = A.twN[i];
   if constexpr (LT) {  // [m/2][l][m&1] = W_P^{(l%8)*m}
     for (int i = threadIdx.x; i < 8 * P; i += WG) {
@@ -212,9 +214,12 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
     const int q = e >> 2, l = q % P, i = (q / P) * 4 + (e & 3);
     s_winv[e] = (i < SH) ? A.winv[l + P * i] : 0.f;
   }
-  if constexpr (GLDS) {
+  if constexpr (GM == 1) {
     const int nr = A.n_rows_lds;
     for (int i = threadIdx.x; i < nr * N; i += WG) s_gain[i] = A.gains[i];
+  } else if constexpr (GM == 2) {
+    for (int i = threadIdx.x; i < 2 * N; i += WG)
+      s_gain[i] = A.gains[(int64_t)A.lds_row[i >= N] * N + (i >= N ? i - N : i)];
   }
   __syncthreads();
   const float4* const w4 = reinterpret_cast<const float4*>(s_win);
@@ -292,8 +297,11 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       fft_fwd<P, NR, LT>(v, L, s_twN, s_twP, buf);
       TPROF(2, v[NR - 1].x);
       // ---- gain row (real, even, 1/N folded in), per-lane layout ----
-      if constexpr (GLDS) {
-        const float4* g4 = reinterpret_cast<const float4*>(s_gain + (row ? N : 0));
+      bool g_lds = GM == 1;
+      if constexpr (GM == 2) g_lds = row == A.lds_row[0] || row == A.lds_row[1];
+      if (g_lds) {
+        const float4* g4 =
+            reinterpret_cast<const float4*>(s_gain + ((GM == 1 ? row : row == A.lds_row[1]) ? N : 0));
   #pragma unroll
         for (int n4 = 0; n4 < NR / 4; ++n4) {
           const float4 g = g4[n4 * P + L];
@@ -302,7 +310,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
           v[4 * n4 + 2] = cscale(v[4 * n4 + 2], g.z);
           v[4 * n4 + 3] = cscale(v[4 * n4 + 3], g.w);
         }
-      } else {
+      } else if constexpr (GM != 1) {
         const __amdgpu_buffer_rsrc_t rg = mk_rsrc(A.gains + (int64_t)row * N, N * 4);
   #pragma unroll
         for (int n4 = 0; n4 < NR / 4; ++n4) {
@@ -820,18 +828,20 @@ __global__ __launch_bounds__(256) void k_ola_gather_lds(LdsArgs A) {
 
 template <int P, int NR, int SH, bool PF, bool NT, int WG>
 void launch_main_pf(const MainArgs& A, int ch, hipStream_t s) {
-  const bool gl = A.n_rows_lds > 0;
+  const int gm = A.n_rows_lds > 0 ? (A.lds_mixed ? 2 : 1) : 0;
   const dim3 g((A.n_runs + WG / P - 1) / (WG / P)), b(WG);
 #ifdef TM_DEV_ONE_KERNEL  // asm studies: one instantiation (stereo, LDS gains, WG 256)
-  if constexpr (WG == 256) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, true, PF, NT, WG>), g, b, 0, s, A);
+  if constexpr (WG == 256) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 1, PF, NT, WG>), g, b, 0, s, A);
   return;
 #endif
   if (ch == 2) {
-    if (gl) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, true, PF, NT, WG>), g, b, 0, s, A);
-    else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, false, PF, NT, WG>), g, b, 0, s, A);
+    if (gm == 1) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 1, PF, NT, WG>), g, b, 0, s, A);
+    else if (gm == 2) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 2, PF, NT, WG>), g, b, 0, s, A);
+    else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 0, PF, NT, WG>), g, b, 0, s, A);
   } else {
-    if (gl) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, true, PF, NT, WG>), g, b, 0, s, A);
-    else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, false, PF, NT, WG>), g, b, 0, s, A);
+    if (gm == 1) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, 1, PF, NT, WG>), g, b, 0, s, A);
+    else if (gm == 2) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, 2, PF, NT, WG>), g, b, 0, s, A);
+    else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, 0, PF, NT, WG>), g, b, 0, s, A);
   }
 }
 template <int P, int NR, int SH>

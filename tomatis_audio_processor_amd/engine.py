@@ -17,6 +17,7 @@ Reference behaviour reproduced per mode (file:line):
 from __future__ import annotations
 
 import ctypes as C
+import time
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
@@ -460,16 +461,26 @@ class AdaptivePipeline:
         self.t_out = torch.empty(max(1, ss.n_streams), dtype=torch.float64, device=dev)
         self.peaks = torch.zeros(max(1, self.plan.total_chunks), dtype=torch.int32, device=dev)
         self.inpk = torch.zeros(max(1, ss.n_streams), dtype=torch.int32, device=dev)
-        self._lv_pin = None   # page-locked staging of the host levels (allocated once)
+        self._lv_pin = None   # page-locked staging of r and the host levels (allocated once)
+        self._tlh = torch.empty(3 * max(1, ss.n_streams), dtype=torch.float64, device=dev)
         self.gains = torch.from_numpy(np.stack(rows)).to(dev)
         self.n_rows = len(rows)
         self.out_offs = out_offs
 
-    def run(self, marks=None):
+    def run(self, marks=None, timer=None):
+        """``timer`` (a dict) collects synchronised wall-clock phases (profiling)."""
         torch = _torch()
         L, P, hs = lib(), self.plan.h, stream_handle()
         ss = self.ss
         sts = self.plan.streams
+        t0 = [time.perf_counter()]
+
+        def phase(name):
+            if timer is not None:
+                torch.cuda.synchronize()
+                t = time.perf_counter()
+                timer[name] = timer.get(name, 0.0) + t - t0[0]
+                t0[0] = t
         # 1. input peak per stream -> attenuation (process_tomatis_adaptive.py:201-215)
         self.inpk.zero_()
         check(L.tomatis_absmax_streams(P, ptr(ss.x), ptr(self.inpk), hs), "absmax_streams")
@@ -487,54 +498,49 @@ class AdaptivePipeline:
                 sts[i].in_scale, sts[i].out_scale = 1.0, 1.0
                 prec.append(F64)
         self.plan.update()
+        phase("peak+atten")
         # 2. per-frame levels (f32 and/or f64 r), host log10 exactly as numpy
         if F32 in prec:
             check(L.tomatis_levels(P, ptr(ss.x), ptr(self.r32), F32, hs), "levels f32")
         if F64 in prec:
             check(L.tomatis_levels(P, ptr(ss.x), ptr(self.r64), F64, hs), "levels f64")
-        Ft = self.plan.total_frames
-        r32 = self.r32.cpu().numpy()[:Ft] if F32 in prec else None
-        r64 = self.r64.cpu().numpy()[:Ft] if F64 in prec else None
+        phase("levels_kernel")
         # levels of every frame by the same elementwise numpy call as the
-        # reference's per-frame one (threaded slices), straight into the
-        # page-locked staging block of the upload; then per-stream statistics
+        # reference's per-frame one (threaded slices), r downloaded into and
+        # levels written into page-locked blocks; per-stream order statistics
+        # (p5, p95, median of the valid levels) then on the device
+        Ft = self.plan.total_frames
         if self._lv_pin is None:
             self._lv_pin = torch.empty(max(1, Ft), dtype=torch.float64, pin_memory=True)
+            self._r_pin = {F32: torch.empty(max(1, Ft), dtype=torch.float32, pin_memory=True),
+                           F64: torch.empty(max(1, Ft), dtype=torch.float64, pin_memory=True)}
         lv = self._lv_pin.numpy()[:Ft]
-        if r64 is None:
-            _levels_threaded(r32, lv)
-        elif r32 is None:
-            _levels_threaded(r64, lv)
+        for pr, rd in ((F32, self.r32), (F64, self.r64)):
+            if pr in prec:
+                self._r_pin[pr][:Ft].copy_(rd[:Ft], non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        rs = {pr: self._r_pin[pr].numpy()[:Ft] for pr in (F32, F64) if pr in prec}
+        phase("r_d2h")
+        if len(rs) == 1:
+            _levels_threaded(next(iter(rs.values())), lv)
         else:
             lv32 = np.empty(Ft, np.float64)
             lv64 = np.empty(Ft, np.float64)
-            _levels_threaded(r32, lv32)
-            _levels_threaded(r64, lv64)
+            _levels_threaded(rs[F32], lv32)
+            _levels_threaded(rs[F64], lv64)
             for i in range(ss.n_streams):
                 a, F = sts[i].frame_base, sts[i].n_frames
                 lv[a:a + F] = (lv32 if prec[i] == F32 else lv64)[a:a + F]
-        tlh = np.empty((ss.n_streams, 3), np.float64)
-
-        def stream_stats(i):  # numpy releases the GIL in partition
-            a, F = sts[i].frame_base, sts[i].n_frames
-            lvi = lv[a:a + F]
-            valid = lvi[lvi > -70]
-            if len(valid) == 0:
-                tlh[i] = (np.nan, np.nan, np.median(lvi) if F else 0.0)
-            else:
-                tlh[i] = dsp.level_stats(valid)
-
-        if ss.n_streams > 1:
-            list(_host_pool().map(stream_stats, range(ss.n_streams)))
-        else:
-            stream_stats(0)
+        phase("log10")
         self.levels[:Ft].copy_(self._lv_pin[:Ft], non_blocking=True)
-        tl = torch.from_numpy(tlh.reshape(-1)).to(self.levels.device)
-        self._tlh = tl
+        tl = self._tlh
+        check(L.tomatis_level_stats(P, ptr(self.levels), ptr(tl), hs), "level_stats")
+        phase("upload+stats")
         # 3. bisection + min-hold states + alpha + rows
         check(L.tomatis_minhold_bisect(P, ptr(self.levels), ptr(tl), self.target_c2,
                                        self.hyst_db, ptr(self.t_out), ptr(self.states),
                                        ptr(self.rows), ptr(self.alpha), hs), "minhold_bisect")
+        phase("bisect+minhold")
         # 4. STFT-gain-OLA, normalise max(w,1e-8), restore, global limiter (one
         #    chunk per stream: fused into the transform when its runs allow)
         self.peaks.zero_()
@@ -545,6 +551,7 @@ class AdaptivePipeline:
                                          PEAK_LIMIT, hs), "stft_ola_limited")
         if marks:
             marks[1].record()
+        phase("transform+limiter")
         self.prec = prec
         return self.result()
 
