@@ -178,6 +178,19 @@ int tomatis_gate_segment_sums(tomatis_plan_t plan, const float* r, int32_t* sums
 int tomatis_gate_std_carry(tomatis_plan_t plan, const float* r, const int32_t* carry_host,
                            uint8_t* states, uint16_t* rows, void* hip_stream);
 
+/* Device-resident time-shard step (timeshard.py; single-stream plans):
+ * tomatis_ts_summary: the gate summary (5 int32, TOMATIS_GATE_NONE for none)
+ *   of the plan's first n_seg gate segments re-indexed by +shift frames, into
+ *   device memory (the all_gather input).  Replaces timeshard.summarize/gs_cat
+ *   on the host.
+ * tomatis_ts_gate: the carry-in composed from sums_all[5*q..] of ranks
+ *   q < rank, re-indexed by shift, then the standard gate from it (as
+ *   tomatis_gate_std_carry, asynchronous, no host data). */
+int tomatis_ts_summary(tomatis_plan_t plan, const float* r, int32_t n_seg, int32_t shift,
+                       int32_t* sum_out, void* hip_stream);
+int tomatis_ts_gate(tomatis_plan_t plan, const float* r, const int32_t* sums_all, int32_t rank,
+                    int32_t shift, uint8_t* states, uint16_t* rows, void* hip_stream);
+
 /* Adaptive: per stream, t_lo_hi_med[3*s..3*s+2] = (np.percentile(v, 5),
  * np.percentile(v, 95), np.median(v)) of v = the stream's levels > -70, or
  * (NaN, NaN, np.median(levels)) when none is valid, (NaN, NaN, 0) for a stream
@@ -218,6 +231,17 @@ int tomatis_apply_limiter(tomatis_plan_t plan, float* y, const uint32_t* chunk_p
 int tomatis_stft_ola_limited(tomatis_plan_t plan, const float* x, const float* gain_rows,
                              int32_t n_rows, const uint16_t* rows, float* y,
                              uint32_t* chunk_peak_bits, float limit, void* hip_stream);
+/* As tomatis_stft_ola_limited, except that the first (edge_mask bit 0) and/or
+ * last (bit 1) limiter chunk of every stream is left unscaled: a time shard's
+ * chunks shared with its neighbours, scaled by tomatis_apply_limiter_edges once
+ * their peaks are all-reduced (src/process_tomatis.py:331-357 per global chunk). */
+int tomatis_stft_ola_limited_edges(tomatis_plan_t plan, const float* x, const float* gain_rows,
+                                   int32_t n_rows, const uint16_t* rows, float* y,
+                                   uint32_t* chunk_peak_bits, float limit, int32_t edge_mask,
+                                   void* hip_stream);
+/* The limiter on the edge chunks of edge_mask only. */
+int tomatis_apply_limiter_edges(tomatis_plan_t plan, float* y, const uint32_t* chunk_peak_bits,
+                                float limit, int32_t edge_mask, void* hip_stream);
 
 /* Synchronous: TOMATIS_E_HIP if a device-side consistency check of the plan's
  * kernels has fired since creation (fused-limiter wait bound), else OK. */

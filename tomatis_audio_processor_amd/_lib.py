@@ -84,6 +84,11 @@ _SIGS = {
     "tomatis_stft_ola": (C.c_int, [_P, _P, _P, C.c_int32, _P, _P, _P, _P]),
     "tomatis_apply_limiter": (C.c_int, [_P, _P, _P, C.c_float, _P]),
     "tomatis_stft_ola_limited": (C.c_int, [_P, _P, _P, C.c_int32, _P, _P, _P, C.c_float, _P]),
+    "tomatis_stft_ola_limited_edges": (C.c_int, [_P, _P, _P, C.c_int32, _P, _P, _P, C.c_float,
+                                                 C.c_int32, _P]),
+    "tomatis_apply_limiter_edges": (C.c_int, [_P, _P, _P, C.c_float, C.c_int32, _P]),
+    "tomatis_ts_summary": (C.c_int, [_P, _P, C.c_int32, C.c_int32, _P, _P]),
+    "tomatis_ts_gate": (C.c_int, [_P, _P, _P, C.c_int32, C.c_int32, _P, _P, _P]),
     "tomatis_plan_error": (C.c_int, [_P, _P]),
     "tomatis_absmax": (C.c_int, [_P, C.c_int64, _P, _P]),
     "tomatis_absmax_streams": (C.c_int, [_P, _P, _P, _P]),

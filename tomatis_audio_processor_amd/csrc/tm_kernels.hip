@@ -491,6 +491,33 @@ __global__ __launch_bounds__(256) void k_gate_states(const float* __restrict__ r
   }
 }
 
+// time shards (timeshard.py): the summary of this shard's first n_seg segments
+// (stream 0) re-indexed by +shift frames; and the carry-in composed from the
+// summaries of ranks 0..rank-1, re-indexed by -shift.  One thread each: a few
+// hundred segments / ranks.
+__device__ __forceinline__ int gs_sh(int v, int off) { return v == kNI ? kNI : v + off; }
+__global__ void k_ts_fold(const GSum* __restrict__ sums, int n_seg, int D, int shift,
+                          int32_t* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  GSum S = gs_identity();
+  for (int i = 0; i < n_seg; ++i) S = gs_cat(S, sums[i], D);
+  out[0] = S.all_on;
+  out[1] = gs_sh(S.not_on, shift);
+  out[2] = gs_sh(S.l_end, shift);
+  out[3] = gs_sh(S.e_int, shift);
+  out[4] = gs_sh(S.off, shift);
+}
+__global__ void k_ts_carry(const int32_t* __restrict__ all, int rank, int D, int shift,
+                           GCarry* __restrict__ carry) {
+  if (threadIdx.x != 0) return;
+  GCarry c{-1, kNI, kNI};
+  for (int q = 0; q < rank; ++q) {
+    const int32_t* v = all + 5 * q;
+    c = gs_apply(c, GSum{v[0], v[1], v[2], v[3], v[4]}, D);
+  }
+  carry[0] = GCarry{c.a + shift, gs_sh(c.e, shift), gs_sh(c.f, shift)};
+}
+
 // ===========================================================================
 // alpha scans (sequential per stream; f64 exactly as the reference)
 // ===========================================================================
@@ -1031,13 +1058,18 @@ struct ChunkDesc {
   int64_t p0, p1;  // output-relative sample range [p0, p1)
 };
 
+// sel 0: every chunk; 1: all but the edge chunks of edge_mask; 2: only those
 __global__ __launch_bounds__(256) void k_limiter(float* __restrict__ y,
                                                  const TomatisStream* __restrict__ st,
                                                  const ChunkDesc* __restrict__ chunks,
                                                  const uint32_t* __restrict__ peaks, float limit,
-                                                 int ch) {
+                                                 int ch, int sel, int edge_mask) {
   const ChunkDesc C = chunks[blockIdx.y];
   const TomatisStream S = st[C.s];
+  if (sel) {
+    const bool edge = ((edge_mask & 1) && C.c == 0) || ((edge_mask & 2) && C.c == S.n_chunks - 1);
+    if (edge != (sel == 2)) return;
+  }
   const float peak = __uint_as_float(peaks[S.chunk_base + C.c]);
   if (!(peak > limit)) return;
   const float sc = limit / peak;
@@ -1220,6 +1252,8 @@ struct tomatis_plan_s {
   int64_t* chunk_rng = nullptr;
   uint32_t* err = nullptr;
   int fuse_span = 0;  // max runs contributing to one chunk
+  int64_t run_slots = 0;  // resident sequences of the fused kernel
+  int edge_mask = 0;      // set for one tomatis_stft_ola_limited_edges call
   // run-scan gate (exclusive on/off predicates)
   bool gate_excl = false;
   void* gsum = nullptr;
@@ -1364,20 +1398,31 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
     e_hi[s] = hi;
     fast_total += hi - lo;
   }
-  int T = env_int("TOMATIS_RUN_FRAMES", 0);
-  if (T <= 0) {
+  // resident sequence slots of the fused kernel
+  int64_t slots;
+  {
     int dev = 0, ncu = 256;
     if (hipGetDevice(&dev) == hipSuccess)
       (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    const int64_t slots = (int64_t)std::max(1, ncu) *
-                          (p->generic ? 8 : transform_slots_per_cu(P, p->NR));
+    slots = (int64_t)std::max(1, ncu) * (p->generic ? 8 : transform_slots_per_cu(P, p->NR));
+  }
+  p->run_slots = slots;
+  // rounds: the runs fill the slots this many times over, in stream/position
+  // order, so (in-order dispatch) early streams and chunks complete while later
+  // runs still compute, and their limiter rescale overlaps that compute
+  // (adaptive: every stream is one limiter chunk, measured 1.4 ms faster on C3
+  // with 2 rounds; standard 10 s chunks gain nothing and pay warm-up frames)
+  const int rounds =
+      std::max(1, env_int("TOMATIS_RUN_ROUNDS", (d.alpha_mode == 2 && ns > 1) ? 2 : 1));
+  int T = env_int("TOMATIS_RUN_FRAMES", 0);
+  if (T <= 0) {
     // generic streams and the edge runs take slots first
     int64_t gen_frames = 0;
     for (int s = 0; s < ns; ++s)
       if (e_lo[s] == e_hi[s]) gen_frames += p->hs[s].n_frames;
     const int64_t work = fast_total + gen_frames;
-    const int64_t avail = std::max<int64_t>(1, slots - n_edge);
-    T = (int)std::max<int64_t>(48, (work + avail - 1) / avail);
+    const int64_t avail = std::max<int64_t>(1, rounds * slots - n_edge);
+    T = (int)std::max<int64_t>(rounds > 1 ? 32 : 48, (work + avail - 1) / avail);
     auto count = [&](int64_t t) {
       int64_t c = n_edge;
       for (int s = 0; s < ns; ++s) {
@@ -1386,7 +1431,7 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
       }
       return c;
     };
-    while (count(T) > slots && T < tf_total) T += std::max(1, T / 64);
+    while (count(T) > rounds * slots && T < tf_total) T += std::max(1, T / 64);
   }
   T = std::min(T, 1 << 20);  // interior buffer resources stay far below 4 GB
   std::vector<Run> runs;
@@ -1884,6 +1929,40 @@ int tomatis_gate_std_carry(tomatis_plan_t p, const float* r, const int32_t* carr
   return hipfail(hipStreamSynchronize(s));  // carry_host may be reused by the caller
 }
 
+int tomatis_ts_summary(tomatis_plan_t p, const float* r, int32_t n_seg, int32_t shift,
+                       int32_t* sum_out, void* hs) {
+  if (!p || !r || !sum_out || n_seg < 0) return TOMATIS_E_ARG;
+  if (!p->gate_excl || p->n_streams != 1) return TOMATIS_E_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)hs;
+  const int D = p->d.up_delay_frames;
+  if (p->n_segs > 0)
+    hipLaunchKernelGGL(k_gate_sum, dim3(p->n_segs), dim3(256), 0, s, r, p->st, p->segs, D,
+                       (GSum*)p->gsum);
+  hipLaunchKernelGGL(k_ts_fold, dim3(1), dim3(64), 0, s, (const GSum*)p->gsum,
+                     std::min<int>(n_seg, p->n_segs), D, shift, sum_out);
+  return launch_check();
+}
+
+int tomatis_ts_gate(tomatis_plan_t p, const float* r, const int32_t* sums_all, int32_t rank,
+                    int32_t shift, uint8_t* states, uint16_t* rows, void* hs) {
+  if (!p || !r || !sums_all || rank < 0 || !states || !rows) return TOMATIS_E_ARG;
+  if (!p->gate_excl || p->d.alpha_mode != 0 || p->n_streams != 1) return TOMATIS_E_UNSUPPORTED;
+  if (p->n_segs == 0) return TOMATIS_OK;
+  hipStream_t s = (hipStream_t)hs;
+  if (!p->gcarry_in && hipMalloc(&p->gcarry_in, sizeof(GCarry))) return TOMATIS_E_NOMEM;
+  const int D = p->d.up_delay_frames;
+  hipLaunchKernelGGL(k_ts_carry, dim3(1), dim3(64), 0, s, sums_all, rank, D, shift,
+                     (GCarry*)p->gcarry_in);
+  hipLaunchKernelGGL(k_gate_sum, dim3(p->n_segs), dim3(256), 0, s, r, p->st, p->segs, D,
+                     (GSum*)p->gsum);
+  hipLaunchKernelGGL(k_gate_carry, dim3(p->n_streams), dim3(256), 0, s, p->seg_first,
+                     p->seg_count, D, (const GSum*)p->gsum, (GCarry*)p->gcarry,
+                     (const GCarry*)p->gcarry_in);
+  hipLaunchKernelGGL(k_gate_states, dim3(p->n_segs), dim3(256), 0, s, r, p->st, p->segs, D,
+                     (const GCarry*)p->gcarry, states, rows);
+  return launch_check();
+}
+
 int tomatis_level_stats(tomatis_plan_t p, const double* levels, double* tlh, void* hs) {
   if (!p || !levels || !tlh) return TOMATIS_E_ARG;
   if (p->n_streams == 0) return TOMATIS_OK;
@@ -1972,6 +2051,7 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
   A.inv_n = 1.0f / (float)N;
   A.n_rows_lds = (n_rows <= 2 && N <= 2048) ? n_rows : 0;
   A.lds_mixed = 0;
+  A.edge_mask = p->edge_mask;
   A.lds_row[0] = 0;
   A.lds_row[1] = 1;
   if (n_rows > 2 && N <= 2048 && p->d.alpha_mode != 0 && env_int("TOMATIS_GAIN_LDS", 1) != 0) {
@@ -2034,19 +2114,48 @@ int tomatis_stft_ola(tomatis_plan_t p, const float* x, const float* gains, int32
 }
 
 // chunks whose flushes come from at most this many consecutive runs are limited
-// inside the main kernel (waves wait only on near neighbours)
+// inside the main kernel (waves wait only on near neighbours).
+// Runs are dispatched in order and a wave waits only for runs of its own
+// chunks, so at most one chunk is partly dispatched while its waves wait: any
+// span up to the resident slots progresses; half of them keeps a margin.
 constexpr int kFuseMaxSpan = 64;
+static int64_t fuse_max_span(const tomatis_plan_s* p) {
+  return std::max<int64_t>(kFuseMaxSpan, p->run_slots / 2);
+}
+
+static int limiter_launch(tomatis_plan_t p, float* y, const uint32_t* peaks, float limit,
+                          int sel, int edge_mask, void* hs) {
+  if (!p || !y || !peaks) return TOMATIS_E_ARG;
+  if (p->n_chunkdesc == 0) return TOMATIS_OK;
+  const int64_t per = p->max_chunk * p->d.ch;
+  const unsigned gx = (unsigned)std::min<int64_t>(std::max<int64_t>(1, (per + 1023) / 1024), 4096);
+  hipLaunchKernelGGL(k_limiter, dim3(gx, p->n_chunkdesc), dim3(256), 0, (hipStream_t)hs, y, p->st,
+                     p->chunks, peaks, limit, p->d.ch, sel, edge_mask);
+  return launch_check();
+}
+
+int tomatis_stft_ola_limited_edges(tomatis_plan_t p, const float* x, const float* gains,
+                                   int32_t n_rows, const uint16_t* rows, float* y,
+                                   uint32_t* peaks, float limit, int32_t edge_mask, void* hs) {
+  if (!p || !(limit > 0.f) || edge_mask < 0 || edge_mask > 3) return TOMATIS_E_ARG;
+  const bool fuse = !p->generic && p->chunk_done && p->fuse_span > 0 &&
+                    p->fuse_span <= fuse_max_span(p) && env_int("TOMATIS_FUSE_LIMITER", 1) != 0;
+  p->edge_mask = edge_mask;
+  int rc;
+  if (fuse) {
+    rc = stft_ola_impl(p, x, gains, n_rows, rows, y, peaks, limit, hs);
+  } else {
+    rc = stft_ola_impl(p, x, gains, n_rows, rows, y, peaks, 0.f, hs);
+    if (!rc) rc = limiter_launch(p, y, peaks, limit, edge_mask ? 1 : 0, edge_mask, hs);
+  }
+  p->edge_mask = 0;
+  return rc;
+}
 
 int tomatis_stft_ola_limited(tomatis_plan_t p, const float* x, const float* gains,
                              int32_t n_rows, const uint16_t* rows, float* y, uint32_t* peaks,
                              float limit, void* hs) {
-  if (!p || !(limit > 0.f)) return TOMATIS_E_ARG;
-  const bool fuse = !p->generic && p->chunk_done && p->fuse_span > 0 &&
-                    p->fuse_span <= kFuseMaxSpan && env_int("TOMATIS_FUSE_LIMITER", 1) != 0;
-  if (fuse) return stft_ola_impl(p, x, gains, n_rows, rows, y, peaks, limit, hs);
-  int rc = stft_ola_impl(p, x, gains, n_rows, rows, y, peaks, 0.f, hs);
-  if (rc) return rc;
-  return tomatis_apply_limiter(p, y, peaks, limit, hs);
+  return tomatis_stft_ola_limited_edges(p, x, gains, n_rows, rows, y, peaks, limit, 0, hs);
 }
 
 int tomatis_plan_error(tomatis_plan_t p, void* hs) {
@@ -2058,13 +2167,13 @@ int tomatis_plan_error(tomatis_plan_t p, void* hs) {
 }
 
 int tomatis_apply_limiter(tomatis_plan_t p, float* y, const uint32_t* peaks, float limit, void* hs) {
-  if (!p || !y || !peaks) return TOMATIS_E_ARG;
-  if (p->n_chunkdesc == 0) return TOMATIS_OK;
-  const int64_t per = p->max_chunk * p->d.ch;
-  const unsigned gx = (unsigned)std::min<int64_t>(std::max<int64_t>(1, (per + 1023) / 1024), 4096);
-  hipLaunchKernelGGL(k_limiter, dim3(gx, p->n_chunkdesc), dim3(256), 0, (hipStream_t)hs, y, p->st,
-                     p->chunks, peaks, limit, p->d.ch);
-  return launch_check();
+  return limiter_launch(p, y, peaks, limit, 0, 0, hs);
+}
+
+int tomatis_apply_limiter_edges(tomatis_plan_t p, float* y, const uint32_t* peaks, float limit,
+                                int32_t edge_mask, void* hs) {
+  if (edge_mask == 0) return p && y && peaks ? TOMATIS_OK : TOMATIS_E_ARG;
+  return limiter_launch(p, y, peaks, limit, 2, edge_mask & 3, hs);
 }
 
 int tomatis_absmax(const float* x, int64_t n, uint32_t* out, void* hs) {

@@ -45,6 +45,7 @@ struct MainArgs {
   int n_runs, hop, n_bins, ch, norm_mode, rmax, n_rows_lds;
   int lds_row[2];       // GM 2: the rows held in LDS (others read from global)
   int lds_mixed;        // 1: n_rows > 2, only lds_row[] in LDS
+  int edge_mask;        // fused limiter skips chunk 0 (bit 0) / the last chunk (bit 1)
   float inv_n;
   // fused limiter (limit > 0): per-chunk flush counters, flushes expected,
   // output ranges; every wave rescales its own output once its chunks are final

@@ -587,8 +587,12 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
     const int nw = P / 64, w = L >> 6;
     const int64_t span = hi - lo, per = (span + nw - 1) / nw;
     const int64_t wlo = lo + per * w, whi = min(hi, wlo + per);
-    for (int c = cid_first; c <= cid; ++c)
+    for (int c = cid_first; c <= cid; ++c) {
+      // edge chunks (shared with a neighbouring time shard) are scaled after
+      // the peak exchange instead (tomatis_apply_limiter_edges)
+      if (((A.edge_mask & 1) && c == 0) || ((A.edge_mask & 2) && c == S.n_chunks - 1)) continue;
       limit_own<CH>(A, S, S.chunk_base + c, wlo, whi, L & 63);
+    }
   }
 #ifdef TM_PROFILE
   if (valid && (R.last & kRunInterior) && L == 0) {

@@ -131,6 +131,7 @@ class Shard:
     p1: int
     geometry: Dict = field(default_factory=dict)   # GatePipeline geometry (local)
     chunk_lo: int = 0                              # global index of local chunk 0
+    edge_mask: int = 0    # bit 0: local chunk 0 shared with rank-1; bit 1: last with rank+1
 
 
 def plan_shards(N: int, n_fft: int, hop: int, world: int, seg: int = GATE_SEGMENT,
@@ -181,8 +182,10 @@ def plan_shards(N: int, n_fft: int, hop: int, world: int, seg: int = GATE_SEGMEN
                     chunk_len=chunk_len if n_loc > 1 else 1,
                     bounds=[max(p0, bounds[c]) - lo for c in range(c_lo, c_hi + 1)] + [p1 - lo])
         tf = (bs[r + 1] - b) if not last else (kl - b + 1)
+        edge = (1 if r > 0 and chunk_of(p0 - 1) == c_lo else 0) | \
+               (2 if not last and chunk_of(p1) == c_hi else 0)
         shards.append(Shard(rank=r, world=R, b=b, k0=k0, k1=k1, tf_frames=tf, lo=lo, hi=hi,
-                            p0=p0, p1=p1, geometry=geom, chunk_lo=c_lo))
+                            p0=p0, p1=p1, geometry=geom, chunk_lo=c_lo, edge_mask=edge))
     return shards
 
 
@@ -195,12 +198,15 @@ def n_chunks_global(N: int, n_fft: int, hop: int, flush: int = 48000 * 5) -> int
 # ---------------------------------------------------------------------------
 
 class ShardRunner:
-    """The standard pipeline on one shard: levels -> gate summary | exchange |
-    gate from carry -> transform + chunk peaks | exchange | limiter fix-up."""
+    """The standard pipeline on one shard, device-resident end to end:
+    levels -> gate summary (5 int32 on the device) | all_gather | carry-in and
+    gate -> transform with the limiter fused for this shard's own chunks |
+    all_reduce(MAX) of the shared edge chunks' peaks | limiter on those."""
 
     def __init__(self, x_slice, sr: int, shard: Shard, ch: int = 2, **params):
         """``x_slice``: the shard's input samples [lo, hi), host [n, ch] array or
         flat device float32 tensor (interleaved)."""
+        import torch
         from . import engine
         self.shard = shard
         if hasattr(x_slice, "data_ptr"):
@@ -208,87 +214,83 @@ class ShardRunner:
         else:
             ss = engine.StreamSet.from_arrays([x_slice], sr)
         self.pipe = engine.GatePipeline(ss, geometry=[shard.geometry], **params)
+        self.sum5 = torch.empty(5, dtype=torch.int32, device=ss.x.device)
+        self.n_chunks = shard.geometry["n_chunks"]
 
     # phase 1
     def summary(self):
-        """Levels, then this rank's gate summary in global frame indices."""
-        import ctypes as C
+        """Levels, then this rank's gate summary in global frame indices
+        (device int32[5], the all_gather input)."""
         from ._lib import check, lib, ptr, stream_handle, F32
         L, P, hs = lib(), self.pipe.plan.h, stream_handle()
         check(L.tomatis_levels(P, ptr(self.pipe.ss.x), ptr(self.pipe.r), F32, hs), "levels")
-        nseg = int(L.tomatis_plan_gate_segments(P))
-        buf = np.zeros((max(1, nseg), 5), np.int32)
-        check(L.tomatis_gate_segment_sums(P, ptr(self.pipe.r),
-                                          buf.ctypes.data_as(C.c_void_p), hs), "gate_segment_sums")
-        D = self.pipe.up_delay_frames
         n_tf_segs = -(-self.shard.tf_frames // GATE_SEGMENT)
-        S = gs_identity()
-        for i in range(min(n_tf_segs, nseg)):
-            S = gs_cat(S, tuple(int(v) for v in buf[i]), D)
-        self.local_sums = buf[:nseg]
-        return gs_shift(S, self.shard.b)
+        check(L.tomatis_ts_summary(P, ptr(self.pipe.r), n_tf_segs, self.shard.b, ptr(self.sum5),
+                                   hs), "ts_summary")
+        return self.sum5
 
     # phase 2
-    def gate_and_transform(self, summaries_global, marks=None):
-        """Gate from the composed carry, then the transform; returns the local
-        chunk peaks (uint32 float bits) placed in a global chunk array."""
-        import ctypes as C
-        from ._lib import check, lib, ptr, stream_handle
-        L, P, hs = lib(), self.pipe.plan.h, stream_handle()
-        D = self.pipe.up_delay_frames
-        c = carry_shift(carry_in(summaries_global, self.shard.rank, D), -self.shard.b)
-        carry = np.asarray(c, np.int32)
-        pp = self.pipe
-        check(L.tomatis_gate_std_carry(P, ptr(pp.r), carry.ctypes.data_as(C.c_void_p),
-                                       ptr(pp.states), ptr(pp.rows), hs), "gate_std_carry")
-        pp.peaks.zero_()
-        if marks:
-            marks[0].record()
-        check(L.tomatis_stft_ola(P, ptr(pp.ss.x), ptr(pp.gains), pp.n_rows, ptr(pp.rows),
-                                 ptr(pp.y), ptr(pp.peaks), hs), "stft_ola")
-        if marks:
-            marks[1].record()
-        return pp.peaks
-
-    # phase 3
-    def limit(self, peaks_local):
+    def gate_and_transform(self, sums_all, marks=None):
+        """Gate from the carry composed of ``sums_all`` (device int32[5 * world],
+        rank order), then the transform; own chunks limited in the kernel.
+        Returns the local chunk peaks (device, uint32 float bits as int32)."""
         from ._lib import check, lib, ptr, stream_handle
         from .engine import PEAK_LIMIT
         L, P, hs = lib(), self.pipe.plan.h, stream_handle()
         pp = self.pipe
-        pp.peaks.copy_(peaks_local)
-        check(L.tomatis_apply_limiter(P, ptr(pp.y), ptr(pp.peaks), PEAK_LIMIT, hs), "limiter")
+        check(L.tomatis_ts_gate(P, ptr(pp.r), ptr(sums_all), self.shard.rank, -self.shard.b,
+                                ptr(pp.states), ptr(pp.rows), hs), "ts_gate")
+        pp.peaks.zero_()
+        if marks:
+            marks[0].record()
+        check(L.tomatis_stft_ola_limited_edges(P, ptr(pp.ss.x), ptr(pp.gains), pp.n_rows,
+                                               ptr(pp.rows), ptr(pp.y), ptr(pp.peaks), PEAK_LIMIT,
+                                               self.shard.edge_mask, hs), "stft_ola_limited_edges")
+        if marks:
+            marks[1].record()
+        return pp.peaks[:self.n_chunks]
+
+    # phase 3
+    def limit_edges(self):
+        """Limiter on the shared edge chunks, whose exchanged peaks are in
+        ``pipe.peaks``."""
+        from ._lib import check, lib, ptr, stream_handle
+        from .engine import PEAK_LIMIT
+        pp = self.pipe
+        check(lib().tomatis_apply_limiter_edges(pp.plan.h, ptr(pp.y), ptr(pp.peaks), PEAK_LIMIT,
+                                                self.shard.edge_mask, stream_handle()),
+              "limiter_edges")
         return pp.result()
 
 
 def run_emulated(x: np.ndarray, sr: int, world: int, **params):
-    """All shards of one stream in this process, exchanges done on the host.
-    Returns (y [N, ch], states [F], per-chunk peaks as float) — the same values
-    a ``world``-rank run produces."""
+    """All shards of one stream in this process, the exchanges done with device
+    tensor ops.  Returns (y [N, ch], states [F], per-chunk peaks as float) — the
+    same values a ``world``-rank run produces."""
     import torch
     N, ch = x.shape
     n_fft, hop = params["n_fft"], params["hop"]
     shards = plan_shards(N, n_fft, hop, world)
     runners = [ShardRunner(x[s.lo:s.hi], sr, s, ch=ch, **params) for s in shards]
-    sums = [rn.summary() for rn in runners]
+    sums_all = torch.cat([rn.summary() for rn in runners])
     G = n_chunks_global(N, n_fft, hop)
-    gpk = np.zeros(G, np.uint32)
-    loc = []
+    gpk = torch.zeros(G, dtype=torch.int32, device=sums_all.device)
     for rn in runners:
-        pk = rn.gate_and_transform(sums).cpu().numpy().astype(np.uint32)
-        n = rn.shard.geometry["n_chunks"]
-        c0 = rn.shard.chunk_lo
-        gpk[c0:c0 + n] = np.maximum(gpk[c0:c0 + n], pk[:n])
-        loc.append((c0, n))
+        pk = rn.gate_and_transform(sums_all)
+        c0, n = rn.shard.chunk_lo, rn.n_chunks
+        gpk[c0:c0 + n] = torch.maximum(gpk[c0:c0 + n], pk)
     ys, sts = [], []
-    for rn, (c0, n) in zip(runners, loc):
-        res = rn.limit(torch.from_numpy(gpk[c0:c0 + n].astype(np.int32)).to(rn.pipe.peaks.device))
+    for rn in runners:
+        c0, n = rn.shard.chunk_lo, rn.n_chunks
+        rn.pipe.peaks[:n].copy_(gpk[c0:c0 + n])
+        res = rn.limit_edges()
         ys.append(res.output(0))
         s = rn.shard
         st = res.stream_states(0)
         sts.append(st[s.k0 - s.b:s.k1 - s.b])
     torch.cuda.synchronize()
-    return np.concatenate(ys), np.concatenate(sts), gpk.view(np.float32)
+    return (np.concatenate(ys), np.concatenate(sts),
+            gpk.cpu().numpy().astype(np.uint32).view(np.float32))
 
 
 # ---------------------------------------------------------------------------
@@ -296,56 +298,47 @@ def run_emulated(x: np.ndarray, sr: int, world: int, **params):
 # tensors with the nccl backend, gloo on CPU tensors in the tests)
 # ---------------------------------------------------------------------------
 
-def exchange_summaries(S, device=None):
-    """all_gather of this rank's 5-int summary -> list of every rank's."""
+def _world():
+    import torch.distributed as dist
+    return dist.get_world_size() if dist.is_initialized() else 1
+
+
+def all_gather_cat(t):
+    """Concatenation of every rank's tensor ``t`` (rank order)."""
     import torch
     import torch.distributed as dist
-    t = torch.tensor(S, dtype=torch.int64, device=device)
-    if not dist.is_initialized() or dist.get_world_size() == 1:
-        return [tuple(int(v) for v in t.cpu())]
+    if _world() == 1:
+        return t
     out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
     dist.all_gather(out, t)
-    return [tuple(int(v) for v in o.cpu()) for o in out]
+    return torch.cat(out)
+
+
+def all_reduce_max(t):
+    """In-place MAX over ranks (non-negative float bit patterns order as ints)."""
+    import torch.distributed as dist
+    if _world() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t
+
+
+def exchange_summaries(S, device=None):
+    """Host form of the summary exchange: every rank's 5-int summary."""
+    import torch
+    t = all_gather_cat(torch.tensor(S, dtype=torch.int64, device=device))
+    return [tuple(int(v) for v in t[5 * q:5 * q + 5].cpu()) for q in range(t.numel() // 5)]
 
 
 def exchange_peaks(global_bits: np.ndarray, device=None) -> np.ndarray:
-    """all_reduce(MAX) of per-chunk peak bits (non-negative floats order as
-    their bit patterns)."""
+    """Host form of the peak exchange: all_reduce(MAX) of per-chunk peak bits."""
     import torch
-    import torch.distributed as dist
-    t = torch.from_numpy(global_bits.astype(np.int64)).to(device or "cpu")
-    if dist.is_initialized() and dist.get_world_size() > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t = all_reduce_max(torch.from_numpy(global_bits.astype(np.int64)).to(device or "cpu"))
     return t.cpu().numpy().astype(np.uint32)
 
 
-def run_rank(x_slice, sr: int, N: int, rank: int, world: int, ch: int = 2, device="cuda",
-             **params):
-    """This rank's shard of an N-sample stream (``x_slice`` = samples
-    [shard.lo, shard.hi), host array or device tensor).  Returns (shard, Result).
-    Collectives: one all_gather (gate summaries), one all_reduce (chunk peaks)."""
-    import torch
-    n_fft, hop = params["n_fft"], params["hop"]
-    shards = plan_shards(N, n_fft, hop, world)
-    if len(shards) != world:
-        raise ValueError(f"stream too short for {world} shards")
-    sh = shards[rank]
-    rn = ShardRunner(x_slice, sr, sh, ch=ch, **params)
-    sums = exchange_summaries(rn.summary(), device=device)
-    pk = rn.gate_and_transform(sums).cpu().numpy().astype(np.uint32)
-    G = n_chunks_global(N, n_fft, hop)
-    g = np.zeros(G, np.uint32)
-    n = sh.geometry["n_chunks"]
-    g[sh.chunk_lo:sh.chunk_lo + n] = pk[:n]
-    g = exchange_peaks(g, device=device)
-    res = rn.limit(torch.from_numpy(g[sh.chunk_lo:sh.chunk_lo + n].astype(np.int32))
-                   .to(rn.pipe.peaks.device))
-    return sh, res
-
-
 class RankStep:
-    """One rank's shard, set up once; ``run()`` = one pass with both exchanges
-    (bench.py workload c2ts)."""
+    """One rank's shard, set up once; ``run()`` = one pass with both exchanges,
+    device-resident (no host synchronisation): bench.py workload c2ts."""
 
     def __init__(self, x_slice, sr: int, N: int, rank: int, world: int, ch: int = 2,
                  device="cuda", **params):
@@ -356,19 +349,28 @@ class RankStep:
         self.sh = shards[rank]
         self.rn = ShardRunner(x_slice, sr, self.sh, ch=ch, **params)
         self.G = n_chunks_global(N, params["n_fft"], params["hop"])
-        self.device = device
-        self.torch = torch
+        self.gpk = torch.zeros(self.G, dtype=torch.int32, device=device)
 
     def run(self, marks=None):
-        sh, rn = self.sh, self.rn
-        sums = exchange_summaries(rn.summary(), device=self.device)
-        pk = rn.gate_and_transform(sums, marks).cpu().numpy().astype(np.uint32)
-        g = np.zeros(self.G, np.uint32)
-        n = sh.geometry["n_chunks"]
-        g[sh.chunk_lo:sh.chunk_lo + n] = pk[:n]
-        g = exchange_peaks(g, device=self.device)
-        return rn.limit(self.torch.from_numpy(g[sh.chunk_lo:sh.chunk_lo + n].astype(np.int32))
-                        .to(rn.pipe.peaks.device))
+        rn, sh = self.rn, self.sh
+        sums_all = all_gather_cat(rn.summary())
+        pk = rn.gate_and_transform(sums_all, marks)
+        if _world() > 1:
+            c0, n = sh.chunk_lo, rn.n_chunks
+            self.gpk.zero_()
+            self.gpk[c0:c0 + n] = pk
+            all_reduce_max(self.gpk)
+            pk.copy_(self.gpk[c0:c0 + n])
+        return rn.limit_edges()
 
     def result(self):
         return self.rn.pipe.result()
+
+
+def run_rank(x_slice, sr: int, N: int, rank: int, world: int, ch: int = 2, device="cuda",
+             **params):
+    """This rank's shard of an N-sample stream (``x_slice`` = samples
+    [shard.lo, shard.hi), host array or device tensor).  Returns (shard, Result).
+    Collectives: one all_gather (gate summaries), one all_reduce (chunk peaks)."""
+    st = RankStep(x_slice, sr, N, rank, world, ch=ch, device=device, **params)
+    return st.sh, st.run()
