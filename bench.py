@@ -241,7 +241,8 @@ def main():
         pipe = engine.GatePipeline(ss, gate_ui=50, gate_offset=-90, n_fft=n_fft, hop=hop,
                                    xfade_ms=500.0)
     elif mode == "adaptive":
-        pipe = engine.AdaptivePipeline(ss, n_fft=n_fft, hop=hop)
+        # two stream groups: one group's host phase overlaps the other's device work
+        pipe = engine.AdaptiveGroups(ss, groups=2, n_fft=n_fft, hop=hop)
     elif mode == "chain":
         pipe = ChainC5(engine, ss, sr, n_fft, hop)
         stages = 2

@@ -75,7 +75,10 @@ def test_c5_chain_xfade_then_layer2b():
         assert np.abs(y2[m3] - rc["y"][m3]).max() <= 3 * TOL
 
 
-def test_c3_mixed_loudness_batch():
+@pytest.mark.parametrize("groups", [0, 3])
+def test_c3_mixed_loudness_batch(groups):
+    """8 adaptive streams of mixed loudness (f32 and f64 paths in one batch)
+    against the oracle; groups=3: the interleaved AdaptiveGroups driver."""
     torch, E = _engine()
     sr, n_fft, hop = 44100, 2048, 512
     scales = [1.0, 0.01, 1.0, 0.02, 3.0, 0.005, 1.0, 0.01]   # f32 / f64 paths interleaved
@@ -85,10 +88,18 @@ def test_c3_mixed_loudness_batch():
         x = synth_stream(700 + i, n, 2, sr)
         xs.append(np.clip(x * np.float32(s), -1, 1).astype(np.float32) if s != 1.0 else x)
     ss = E.StreamSet.from_arrays(xs, sr)
-    pipe = E.AdaptivePipeline(ss, n_fft=n_fft, hop=hop)
-    res = pipe.run()
-    torch.cuda.synchronize()
-    pipe.plan.check_device()
+    if groups:
+        pipe = E.AdaptiveGroups(ss, groups=groups, n_fft=n_fft, hop=hop)
+        res = pipe.run()
+        torch.cuda.synchronize()
+        assert len(pipe.pipes) == groups
+        for p in pipe.pipes:
+            p.plan.check_device()
+    else:
+        pipe = E.AdaptivePipeline(ss, n_fft=n_fft, hop=hop)
+        res = pipe.run()
+        torch.cuda.synchronize()
+        pipe.plan.check_device()
     prec = res.extra["prec"]
     assert len(set(prec)) == 2, "both precision paths must be in the batch"
     thr = res.extra["thresholds"].cpu().numpy()

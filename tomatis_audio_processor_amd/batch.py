@@ -72,8 +72,9 @@ def run(args):
         offs = list(np.cumsum([0] + [n * ch for n in lens[:-1]]).astype(int))
         del parts
         ss = engine.StreamSet(x=x, offs=offs, lens=lens, ch=ch, sr=sr)
-        if args.mode == "adaptive":
-            pipe = engine.AdaptivePipeline(ss, **params)
+        if args.mode == "adaptive":   # >= 4 files: two interleaved stream groups
+            pipe = (engine.AdaptiveGroups(ss, groups=2, **params) if len(ids) >= 4
+                    else engine.AdaptivePipeline(ss, **params))
         elif args.mode == "xfade":
             pipe = engine.GatePipeline(ss, gate_ui=args.gate_ui, gate_offset=args.gate_offset,
                                        xfade_ms=args.xfade_ms, **params)

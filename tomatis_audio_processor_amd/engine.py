@@ -416,7 +416,9 @@ class AdaptivePipeline:
 
     def __init__(self, ss: StreamSet, *, fc=1000.0, slope=12.0, c1_low=15.0, c1_high=-15.0,
                  c2_low=-15.0, c2_high=15.0, target_c2=0.5, hyst_db=3.0, min_hold_ms=250.0,
-                 xfade_ms=500.0, headroom_margin=2.0, n_fft=4096, hop=2048):
+                 xfade_ms=500.0, headroom_margin=2.0, n_fft=4096, hop=2048, out=None):
+        """``out``: optional (y, offsets) output buffer shared with other
+        pipelines (AdaptiveGroups)."""
         torch = _torch()
         _check_fft(n_fft, hop, ss.ch)
         self.ss, self.n_fft, self.hop = ss, n_fft, hop
@@ -443,7 +445,10 @@ class AdaptivePipeline:
             st.n_chunks, st.chunk_first, st.chunk_len = 1, 0, 1
             st.in_scale, st.out_scale = 1.0, 1.0
             streams.append(st)
-        self.y, out_offs = _alloc_out(torch, [s.out_len for s in streams], ss.ch, ss.x.device)
+        if out is None:
+            self.y, out_offs = _alloc_out(torch, [s.out_len for s in streams], ss.ch, ss.x.device)
+        else:
+            self.y, out_offs = out[0], list(out[1])
         for st, o in zip(streams, out_offs):
             st.out_off = o
         desc = TomatisPlanDesc(n_fft=n_fft, hop=hop, ch=ss.ch, norm_mode=NORM_MAX,
@@ -462,6 +467,9 @@ class AdaptivePipeline:
         self.peaks = torch.zeros(max(1, self.plan.total_chunks), dtype=torch.int32, device=dev)
         self.inpk = torch.zeros(max(1, ss.n_streams), dtype=torch.int32, device=dev)
         self._lv_pin = None   # page-locked staging of r and the host levels (allocated once)
+        self._pk_pin = torch.empty(max(1, ss.n_streams), dtype=torch.int32, pin_memory=True)
+        self.stream = None    # torch stream the pipeline runs on (None: the current one)
+        self.done = torch.cuda.Event()
         self._tlh = torch.empty(3 * max(1, ss.n_streams), dtype=torch.float64, device=dev)
         self.gains = torch.from_numpy(np.stack(rows)).to(dev)
         self.n_rows = len(rows)
@@ -469,11 +477,23 @@ class AdaptivePipeline:
 
     def run(self, marks=None, timer=None):
         """``timer`` (a dict) collects synchronised wall-clock phases (profiling)."""
+        for _ in self.steps(marks, timer):
+            pass
+        return self.result()
+
+    def steps(self, marks=None, timer=None, after=None):
+        """The pass as a generator that yields wherever the host would wait for
+        the device (the input peaks, the frame r) and before the transform, so a
+        driver can interleave several pipelines on their own streams
+        (AdaptiveGroups).  ``after``: a callable giving an event the transform
+        waits for (launch order)."""
         torch = _torch()
-        L, P, hs = lib(), self.plan.h, stream_handle()
+        strm = self.stream or torch.cuda.current_stream()
+        L, P = lib(), self.plan.h
         ss = self.ss
         sts = self.plan.streams
         t0 = [time.perf_counter()]
+        ev = torch.cuda.Event()
 
         def phase(name):
             if timer is not None:
@@ -481,10 +501,17 @@ class AdaptivePipeline:
                 t = time.perf_counter()
                 timer[name] = timer.get(name, 0.0) + t - t0[0]
                 t0[0] = t
+
         # 1. input peak per stream -> attenuation (process_tomatis_adaptive.py:201-215)
-        self.inpk.zero_()
-        check(L.tomatis_absmax_streams(P, ptr(ss.x), ptr(self.inpk), hs), "absmax_streams")
-        pk = self.inpk.cpu().numpy().astype(np.uint32).view(np.float32)
+        with torch.cuda.stream(strm):
+            hs = stream_handle()
+            self.inpk.zero_()
+            check(L.tomatis_absmax_streams(P, ptr(ss.x), ptr(self.inpk), hs), "absmax_streams")
+            self._pk_pin.copy_(self.inpk, non_blocking=True)
+            ev.record()
+        yield
+        ev.synchronize()
+        pk = self._pk_pin.numpy().astype(np.uint32).view(np.float32)
         self.atten, prec = [], []
         for i in range(ss.n_streams):
             peak_db = 20 * np.log10(pk[i] + dsp.EPS)
@@ -497,30 +524,34 @@ class AdaptivePipeline:
             else:              # float64 pipeline: x * 1.0
                 sts[i].in_scale, sts[i].out_scale = 1.0, 1.0
                 prec.append(F64)
-        self.plan.update()
-        phase("peak+atten")
-        # 2. per-frame levels (f32 and/or f64 r), host log10 exactly as numpy
-        if F32 in prec:
-            check(L.tomatis_levels(P, ptr(ss.x), ptr(self.r32), F32, hs), "levels f32")
-        if F64 in prec:
-            check(L.tomatis_levels(P, ptr(ss.x), ptr(self.r64), F64, hs), "levels f64")
-        phase("levels_kernel")
-        # levels of every frame by the same elementwise numpy call as the
-        # reference's per-frame one (threaded slices), r downloaded into and
-        # levels written into page-locked blocks; per-stream order statistics
-        # (p5, p95, median of the valid levels) then on the device
         Ft = self.plan.total_frames
         if self._lv_pin is None:
             self._lv_pin = torch.empty(max(1, Ft), dtype=torch.float64, pin_memory=True)
             self._r_pin = {F32: torch.empty(max(1, Ft), dtype=torch.float32, pin_memory=True),
                            F64: torch.empty(max(1, Ft), dtype=torch.float64, pin_memory=True)}
-        lv = self._lv_pin.numpy()[:Ft]
-        for pr, rd in ((F32, self.r32), (F64, self.r64)):
-            if pr in prec:
-                self._r_pin[pr][:Ft].copy_(rd[:Ft], non_blocking=True)
-        torch.cuda.current_stream().synchronize()
-        rs = {pr: self._r_pin[pr].numpy()[:Ft] for pr in (F32, F64) if pr in prec}
+        with torch.cuda.stream(strm):
+            hs = stream_handle()
+            self.plan.update()
+            phase("peak+atten")
+            # 2. per-frame levels (f32 and/or f64 r) -> page-locked host blocks
+            if F32 in prec:
+                check(L.tomatis_levels(P, ptr(ss.x), ptr(self.r32), F32, hs), "levels f32")
+            if F64 in prec:
+                check(L.tomatis_levels(P, ptr(ss.x), ptr(self.r64), F64, hs), "levels f64")
+            phase("levels_kernel")
+            for pr, rd in ((F32, self.r32), (F64, self.r64)):
+                if pr in prec:
+                    self._r_pin[pr][:Ft].copy_(rd[:Ft], non_blocking=True)
+            ev.record()
+        yield
+        ev.synchronize()
         phase("r_d2h")
+        # levels of every frame by the same elementwise numpy call as the
+        # reference's per-frame one, written into the page-locked upload block;
+        # per-stream order statistics (p5, p95, median of the valid levels) then
+        # on the device
+        lv = self._lv_pin.numpy()[:Ft]
+        rs = {pr: self._r_pin[pr].numpy()[:Ft] for pr in (F32, F64) if pr in prec}
         if len(rs) == 1:
             _levels_threaded(next(iter(rs.values())), lv)
         else:
@@ -532,28 +563,35 @@ class AdaptivePipeline:
                 a, F = sts[i].frame_base, sts[i].n_frames
                 lv[a:a + F] = (lv32 if prec[i] == F32 else lv64)[a:a + F]
         phase("log10")
-        self.levels[:Ft].copy_(self._lv_pin[:Ft], non_blocking=True)
-        tl = self._tlh
-        check(L.tomatis_level_stats(P, ptr(self.levels), ptr(tl), hs), "level_stats")
-        phase("upload+stats")
-        # 3. bisection + min-hold states + alpha + rows
-        check(L.tomatis_minhold_bisect(P, ptr(self.levels), ptr(tl), self.target_c2,
-                                       self.hyst_db, ptr(self.t_out), ptr(self.states),
-                                       ptr(self.rows), ptr(self.alpha), hs), "minhold_bisect")
-        phase("bisect+minhold")
-        # 4. STFT-gain-OLA, normalise max(w,1e-8), restore, global limiter (one
-        #    chunk per stream: fused into the transform when its runs allow)
-        self.peaks.zero_()
-        if marks:
-            marks[0].record()
-        check(L.tomatis_stft_ola_limited(P, ptr(ss.x), ptr(self.gains), self.n_rows,
-                                         ptr(self.rows), ptr(self.y), ptr(self.peaks),
-                                         PEAK_LIMIT, hs), "stft_ola_limited")
-        if marks:
-            marks[1].record()
-        phase("transform+limiter")
+        with torch.cuda.stream(strm):
+            hs = stream_handle()
+            self.levels[:Ft].copy_(self._lv_pin[:Ft], non_blocking=True)
+            tl = self._tlh
+            check(L.tomatis_level_stats(P, ptr(self.levels), ptr(tl), hs), "level_stats")
+            phase("upload+stats")
+            # 3. bisection + min-hold states + alpha + rows
+            check(L.tomatis_minhold_bisect(P, ptr(self.levels), ptr(tl), self.target_c2,
+                                           self.hyst_db, ptr(self.t_out), ptr(self.states),
+                                           ptr(self.rows), ptr(self.alpha), hs), "minhold_bisect")
+            phase("bisect+minhold")
+        yield   # (a driver launches every group's statistics before the transforms)
+        with torch.cuda.stream(strm):
+            hs = stream_handle()
+            # 4. STFT-gain-OLA, normalise max(w,1e-8), restore, global limiter (one
+            #    chunk per stream: fused into the transform when its runs allow)
+            self.peaks.zero_()
+            if after is not None and after() is not None:
+                strm.wait_event(after())
+            if marks and marks[0] is not None:
+                marks[0].record()
+            check(L.tomatis_stft_ola_limited(P, ptr(ss.x), ptr(self.gains), self.n_rows,
+                                             ptr(self.rows), ptr(self.y), ptr(self.peaks),
+                                             PEAK_LIMIT, hs), "stft_ola_limited")
+            if marks and marks[1] is not None:
+                marks[1].record()
+            self.done.record()
+            phase("transform+limiter")
         self.prec = prec
-        return self.result()
 
     def result(self) -> Result:
         st = list(self.plan.streams)[:self.ss.n_streams]
@@ -570,6 +608,98 @@ class AdaptivePipeline:
                                  prec=getattr(self, "prec", None), n_fft=self.n_fft,
                                  norm="max", limit=PEAK_LIMIT, limiter_applied=True,
                                  out_begin=[s.out_begin for s in st]))
+
+
+def merge_results(results: Sequence[Result]) -> Result:
+    """One Result over several pipelines' streams (same output buffer y; per-frame
+    and per-chunk arrays concatenated, indices re-based)."""
+    torch = _torch()
+    r0 = results[0]
+    if any(r.y.data_ptr() != r0.y.data_ptr() for r in results):
+        raise ValueError("merge_results: pipelines must share one output buffer")
+    fb, cb, ftot, ctot = [], [], 0, 0
+    for r in results:
+        fb += [ftot + v for v in r.frame_base]
+        cb += [ctot + v for v in r.chunk_base]
+        ftot += int(sum(r.n_frames))
+        ctot += int(sum(r.n_chunks))
+
+    def cat(get, n_of):
+        parts = [get(r)[:n_of(r)] for r in results]
+        return torch.cat(parts) if parts else None
+
+    nf = lambda r: int(sum(r.n_frames))  # noqa: E731
+    nc = lambda r: int(sum(r.n_chunks))  # noqa: E731
+    ns = lambda r: len(r.out_lens)       # noqa: E731
+    ex = dict(r0.extra)
+    ex["levels"] = cat(lambda r: r.extra["levels"], nf)
+    ex["thresholds"] = cat(lambda r: r.extra["thresholds"], ns)
+    for k in ("atten_db", "prec", "out_begin"):
+        ex[k] = [v for r in results for v in (r.extra.get(k) or [])]
+    return Result(y=r0.y, out_offs=[o for r in results for o in r.out_offs],
+                  out_lens=[o for r in results for o in r.out_lens], ch=r0.ch,
+                  frame_base=fb, n_frames=[v for r in results for v in r.n_frames],
+                  first_start=[v for r in results for v in r.first_start], hop=r0.hop,
+                  states=cat(lambda r: r.states, nf), r=cat(lambda r: r.r, nf),
+                  alpha=cat(lambda r: r.alpha, nf), chunk_peaks=cat(lambda r: r.chunk_peaks, nc),
+                  chunk_base=cb, n_chunks=[v for r in results for v in r.n_chunks], extra=ex)
+
+
+class AdaptiveGroups:
+    """An adaptive batch (config C3) as G stream groups, each with its own plan
+    and HIP stream, interleaved so the host phase of one group (peak ->
+    attenuation, numpy log10 of its frame r) overlaps the device work of the
+    others; the transforms launch in group order (each waits for the previous
+    one: a fused-limiter launch never shares the dispatcher with another).
+    Output in one buffer; ``result()`` merges the groups."""
+
+    def __init__(self, ss: StreamSet, groups: int = 2, **params):
+        torch = _torch()
+        n_fft, hop = params.get("n_fft", 4096), params.get("hop", 2048)
+        G = max(1, min(int(groups), ss.n_streams))
+        out_lens = [N if dsp.adaptive_frames(N, n_fft, hop)[1] else 0 for N in ss.lens]
+        self.y, offs = _alloc_out(torch, out_lens, ss.ch, ss.x.device)
+        # contiguous groups balanced by samples
+        tot, acc, cuts = float(sum(ss.lens)) or 1.0, 0, [0]
+        for i, N in enumerate(ss.lens):
+            acc += N
+            if len(cuts) < G and acc >= tot * len(cuts) / G and i + 1 < ss.n_streams:
+                cuts.append(i + 1)
+        cuts.append(ss.n_streams)
+        self.pipes = []
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            sub = StreamSet(x=ss.x, offs=ss.offs[a:b], lens=ss.lens[a:b], ch=ss.ch, sr=ss.sr)
+            p = AdaptivePipeline(sub, out=(self.y, offs[a:b]), **params)
+            p.stream = torch.cuda.Stream()
+            self.pipes.append(p)
+        self.ss = ss
+
+    def run(self, marks=None):
+        torch = _torch()
+        cur = torch.cuda.current_stream()
+        for p in self.pipes:
+            p.stream.wait_stream(cur)
+        G = len(self.pipes)
+        gens = []
+        for g, p in enumerate(self.pipes):
+            mk = None
+            if marks:
+                mk = (marks[0] if g == 0 else None, marks[1] if g == G - 1 else None)
+            prev = self.pipes[g - 1] if g else None
+            gens.append(p.steps(mk, after=(lambda q=prev: q.done) if prev else None))
+        live = list(gens)
+        while live:
+            for gen in list(live):
+                try:
+                    next(gen)
+                except StopIteration:
+                    live.remove(gen)
+        for p in self.pipes:
+            cur.wait_stream(p.stream)
+        return self.result()
+
+    def result(self) -> Result:
+        return merge_results([p.result() for p in self.pipes])
 
 
 # ---------------------------------------------------------------------------
@@ -725,6 +855,6 @@ def _minhold_states(levels, tlhs, hyst_db, mh, target):
     return out
 
 
-__all__ = ["StreamSet", "Plan", "GatePipeline", "AdaptivePipeline", "StaticEqPipeline",
-           "Result", "scale_copy", "frame_r", "compute_frame_levels", "simulate_gate",
+__all__ = ["StreamSet", "Plan", "GatePipeline", "AdaptivePipeline", "AdaptiveGroups", "StaticEqPipeline",
+           "Result", "merge_results", "scale_copy", "frame_r", "compute_frame_levels", "simulate_gate",
            "find_optimal_threshold"]
