@@ -242,7 +242,8 @@ def main():
                                    xfade_ms=500.0)
     elif mode == "adaptive":
         # two stream groups: one group's host phase overlaps the other's device work
-        pipe = engine.AdaptiveGroups(ss, groups=2, n_fft=n_fft, hop=hop)
+        pipe = engine.AdaptiveGroups(ss, groups=int(os.environ.get("TOMATIS_C3_GROUPS", "2")),
+                                     n_fft=n_fft, hop=hop)
     elif mode == "chain":
         pipe = ChainC5(engine, ss, sr, n_fft, hop)
         stages = 2

@@ -146,20 +146,26 @@ def _host_pool():
 
 
 def _levels_threaded(r: np.ndarray, out: np.ndarray):
-    """``dsp.r_to_level(r)`` into ``out`` in slices on the host pool (numpy's
-    elementwise log10 releases the GIL; slicing does not change any value)."""
+    """``dsp.r_to_level(r)`` into ``out``: the same ufunc chain with in-place
+    temporaries (bit-identical: the same loops on the same dtypes), in slices on
+    the host pool when TOMATIS_LOG10_THREADS > 1 (numpy's SIMD log10 does not
+    scale over threads on the measured hosts, so one thread by default)."""
+    import os
     n = len(r)
-    if n < (1 << 16):
-        out[:] = dsp.r_to_level(r)
+    tmp = np.empty(n, np.asarray(r).dtype)
+    k = int(os.environ.get("TOMATIS_LOG10_THREADS", "1"))
+
+    def part(a, b):
+        np.add(r[a:b], dsp.EPS, out=tmp[a:b])
+        np.log10(tmp[a:b], out=tmp[a:b])
+        np.multiply(tmp[a:b], 20.0, out=tmp[a:b])
+        out[a:b] = tmp[a:b]
+
+    if k <= 1 or n < (1 << 16):
+        part(0, n)
         return
-    k = 16
     edges = np.linspace(0, n, k + 1).astype(np.int64)
-
-    def part(i):
-        a, b = edges[i], edges[i + 1]
-        out[a:b] = dsp.r_to_level(r[a:b])
-
-    list(_host_pool().map(part, range(k)))
+    list(_host_pool().map(lambda i: part(edges[i], edges[i + 1]), range(k)))
 
 
 def _set_gate(st: TomatisStream, Ton: float, Toff: float):

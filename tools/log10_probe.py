@@ -48,6 +48,25 @@ def main():
             lambda: list(pool.map(lambda i: inplace(e[i], e[i + 1], o, tmp), range(k))))
         assert np.array_equal(o, ref)
         pool.shutdown()
+    try:   # reading from / writing to page-locked (torch pin_memory) blocks
+        import torch
+        rp = torch.empty(n, dtype=torch.float32, pin_memory=True)
+        op = torch.empty(n, dtype=torch.float64, pin_memory=True)
+        rp.numpy()[:] = r
+        rpn, opn = rp.numpy(), op.numpy()
+        tmp2 = np.empty(n, np.float32)
+
+        def pinned():
+            np.add(rpn, dsp.EPS, out=tmp2)
+            np.log10(tmp2, out=tmp2)
+            np.multiply(tmp2, 20.0, out=tmp2)
+            opn[:] = tmp2
+
+        out["pinned_in_out_ms"] = best(pinned)
+        out["pinned_read_copy_ms"] = best(lambda: np.copy(rpn))
+        out["pinned_write_ms"] = best(lambda: opn.__setitem__(slice(None), o))
+    except Exception as e:  # no ROCm runtime: skip
+        out["pinned"] = str(e)[:80]
     out["cpus"] = len(os.sched_getaffinity(0))
     print(json.dumps(out))
 
