@@ -207,6 +207,9 @@ def main():
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--cpu-sample-s", type=int, default=3600,
                     help="seconds of audio for the 1-core CPU baseline (0 disables the baseline)")
+    ap.add_argument("--input-gain", type=float, default=1.0,
+                    help="scale the synthetic input (e.g. 0.05: no limiter chunk engages; "
+                         "PMC traffic runs)")
     ap.add_argument("--cpu-pool-s", type=int, default=300,
                     help="seconds of audio per worker for the all-cores CPU baseline")
     a = ap.parse_args()
@@ -234,6 +237,8 @@ def main():
         ss = pipe.rn.pipe.ss
     else:
         ss = engine.StreamSet.synthetic(nstr, n, ch, sr, seed0=1000 + rank * nstr)
+        if a.input_gain != 1.0:
+            ss.x = engine.scale_copy(ss.x, a.input_gain)
     stages = 1
     if mode == "standard":
         pipe = engine.GatePipeline(ss, gate_ui=50, n_fft=n_fft, hop=hop)
@@ -308,7 +313,8 @@ def main():
             "value": round(value, 1), "unit": "Msamples/s", "n_gpus": ws, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (seeded device-generated noise, -20/-60 dBFS alternating 1.5 s)",
+            "data": "synthetic (seeded device-generated noise, -20/-60 dBFS alternating 1.5 s)"
+                    + (f", x{a.input_gain:g}" if a.input_gain != 1.0 else ""),
             "config": {"workload": desc, "streams_per_gpu": nstr, "samples_per_channel": n,
                        "channels": ch, "sr": sr, "mode": mode, "n_fft": n_fft, "hop": hop,
                        "parallelism": (f"time-sharded x{ws} (RCCL gate all_gather + peak "

@@ -4,7 +4,7 @@
 set -u
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$PWD}
-OUT=$R/gpurun_out/pmc
+OUT=${PMC_OUT:-$R/gpurun_out/pmc}
 mkdir -p $OUT
 ARGS="bench.py --steps 2 --warmup 1 --cpu-sample-s 0 ${BENCH_ARGS:-}"
 i=0
