@@ -162,6 +162,21 @@ def _decode_flac_ranges(h, torch, buf, size, path, timer):
     return x[:n * ch], n, ch, sr
 
 
+class _EncBuf:
+    """Bytes taken from the streaming encoder: a zero-copy view until free()."""
+
+    def __init__(self, h, p, n):
+        self.h, self.p, self.n = h, p, n
+
+    def view(self):
+        return memoryview((C.c_uint8 * self.n).from_address(C.addressof(self.p.contents)))
+
+    def free(self):
+        if self.p:
+            self.h.tomatis_flac_free(self.p)
+            self.p = None
+
+
 def _encode_segments(y, n, ch, sr, bps, sink, timer=None):
     """Quantise on the device, then per segment of SEG_FRAMES frames: D2H into
     one of two page-locked buffers on a copy stream while the host encodes the
@@ -202,11 +217,9 @@ def _encode_segments(y, n, ch, sr, bps, sink, timer=None):
             _err(h.tomatis_flac_enc_push(enc, pins[k % 2].data_ptr(), b - a),
                  "FLAC encode failed")
             _err(h.tomatis_flac_enc_take(enc, C.byref(out), C.byref(ln)), "FLAC encode failed")
-            if ln.value:
-                try:
-                    sink(C.string_at(out, ln.value))
-                finally:
-                    h.tomatis_flac_free(out)
+            if ln.value:   # the sink owns the encoder buffer (frees it with tomatis_flac_free)
+                sink(_EncBuf(h, out, ln.value))
+                out = C.POINTER(C.c_uint8)()
         hdr = (C.c_uint8 * 42)()
         _err(h.tomatis_flac_enc_header(enc, hdr), "FLAC encode failed")
     finally:
@@ -219,7 +232,14 @@ def _encode_segments(y, n, ch, sr, bps, sink, timer=None):
 def encode_flac_device(y, n: int, ch: int, sr: int, bps: int = 24, timer=None) -> bytes:
     """FLAC stream of the device float32 samples y [n*ch] at ``bps`` bits."""
     parts = []
-    hdr = _encode_segments(y, n, ch, sr, bps, parts.append, timer)
+
+    def take(b):
+        try:
+            parts.append(bytes(b.view()))
+        finally:
+            b.free()
+
+    hdr = _encode_segments(y, n, ch, sr, bps, take, timer)
     return hdr + b"".join(parts)
 
 
@@ -244,9 +264,12 @@ def write_device(out_path: str, y, n: int, ch: int, sr: int, log=print, timer=No
                     if b is None:
                         return
                     try:
-                        f.write(b)
+                        if not err:
+                            f.write(b.view())
                     except Exception as e:  # reported after the encode
                         err.append(e)
+                    finally:
+                        b.free()
 
             th = threading.Thread(target=writer, daemon=True)
             th.start()

@@ -26,6 +26,10 @@ def main():
     d, workload = a[0], a[1]
     kern = a[a.index("--kernel") + 1] if "--kernel" in a else "k_stft_ola"
     alg = float(a[a.index("--alg-bytes") + 1]) if "--alg-bytes" in a else None
+    # reads: "raw" = FETCH_SIZE as reported (8-B-per-lane loads; calibrated on the
+    # limiter-inactive run, whose FETCH_SIZE is 1.08x the input bytes read once),
+    # "x2" = the guide's gfx950 factor for 16-B-per-lane streaming reads
+    reads = a[a.index("--reads") + 1] if "--reads" in a else "raw"
     vals = defaultdict(list)
     for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
@@ -35,7 +39,7 @@ def main():
         sys.exit(f"no FETCH_SIZE/WRITE_SIZE dispatches of {kern} under {d}")
     fetch_kib = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"])
     write_kib = sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"])
-    rd = 2.0 * fetch_kib * 1024.0
+    rd = (2.0 if reads == "x2" else 1.0) * fetch_kib * 1024.0
     wr = write_kib * 1024.0
     out_path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                             "profiles", "pmc_traffic.json")
@@ -45,11 +49,17 @@ def main():
         doc = {}
     rec = {"kernel": kern, "dispatches": len(vals["FETCH_SIZE"]),
            "fetch_size_kib": fetch_kib, "write_size_kib": write_kib,
-           "read_bytes_corrected": rd, "write_bytes": wr,
+           "read_bytes": rd, "write_bytes": wr,
            "hbm_bytes_per_launch": rd + wr,
-           "hbm_bytes_uncorrected": fetch_kib * 1024.0 + wr,
+           "hbm_bytes_x2_reads": 2.0 * fetch_kib * 1024.0 + wr,
            "source": os.path.relpath(d),
-           "correction": "reads = 2 x FETCH_SIZE (gfx950, MI355X_MICROARCH.md HBM section)"}
+           "reads": reads,
+           "correction": ("reads = FETCH_SIZE: the kernel's input loads are 8 B/lane, a width "
+                          "MI355X_MICROARCH.md leaves uncalibrated; calibrated on the "
+                          "limiter-inactive run (bench --input-gain 0.05), where FETCH_SIZE is "
+                          "1.08x the input bytes (each input byte once + warm-up halos)"
+                          if reads == "raw" else
+                          "reads = 2 x FETCH_SIZE (gfx950, 16-B/lane streaming-read factor)")}
     if alg:
         rec["alg_bytes_per_launch"] = alg
         rec["traffic_over_alg"] = (rd + wr) / alg
