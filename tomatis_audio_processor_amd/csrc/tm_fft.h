@@ -72,8 +72,8 @@ __device__ __forceinline__ void fft_fwd(cf (&v)[NR], int L, const cf* twN, const
   constexpr int PB = G::PB, RW = G::RW;
   const int a1 = L & 7, q1 = L >> 3;
   const int c3 = L % PB, q3 = L / PB;
-  // step 1
-  dft<NR, false, 0, 1, NR>(v);
+  // step 1 (outputs carry splan<NR, 0>().sig: the twN table absorbs them)
+  sdft<NR, 0, 0, NR>(v);
   TM_STEP_FENCE();
   // step 2 (twiddles in lane-pair layout: one ds_read_b128 per two registers)
   sfor<0, NR / 2>([&](auto kk) {
@@ -97,10 +97,11 @@ __device__ __forceinline__ void fft_fwd(cf (&v)[NR], int L, const cf* twN, const
     xsync<P>();
   });
   TM_STEP_FENCE();
-  // step 3a: DFT_PB over b for each j
+  // step 3a: DFT_PB over b for each j (output c carries splan<PB, 0>().sig[c],
+  // absorbed by the step-3b twiddles)
   sfor<0, G::NJ>([&](auto jj) {
     constexpr int J = decltype(jj)::value;
-    dft<PB, false, J * PB, 1, NR>(v);
+    sdft<PB, 0, J * PB, NR>(v);
   });
   TM_STEP_FENCE();
   // step 3b: W_P^{a c}
@@ -118,7 +119,8 @@ __device__ __forceinline__ void fft_fwd(cf (&v)[NR], int L, const cf* twN, const
   } else {
     sfor<1, PB>([&](auto cc) {
       constexpr int C = decltype(cc)::value;
-      const cf w = twP[(a1 * C) & (P - 1)];
+      constexpr float sc = (float)splan<PB, 0>().sig[C];
+      const cf w = cscale(twP[(a1 * C) & (P - 1)], sc);
       sfor<0, G::NJ>([&](auto jj) {
         constexpr int J = decltype(jj)::value;
         v[J * PB + C] = cmul(v[J * PB + C], w);
@@ -144,10 +146,11 @@ __device__ __forceinline__ void fft_fwd(cf (&v)[NR], int L, const cf* twN, const
     xsync<P>();
   });
   TM_STEP_FENCE();
-  // step 3c: DFT_8 over a
+  // step 3c: DFT_8 over a (output d carries splan<8, 0>().sig[d], absorbed by
+  // the per-lane gain rows, k_gain_perm)
   sfor<0, NR / 8>([&](auto jj) {
     constexpr int J = decltype(jj)::value;
-    dft<8, false, J * 8, 1, NR>(v);
+    sdft<8, 0, J * 8, NR>(v);
   });
 }
 
@@ -159,10 +162,12 @@ __device__ __forceinline__ void fft_inv(cf (&v)[NR], int L, const cf* twN, const
   constexpr int PB = G::PB, RW = G::RW;
   const int a1 = L & 7, q1 = L >> 3;
   const int c3 = L % PB, q3 = L / PB;
-  // step 3c': IDFT_8 over d -> a
+  // step 3c': IDFT_8 over d -> a (output a carries splan<8, 1>().sig[a] =
+  // splan<8, 0>().sig[a]: absorbed by the scaled step-3b' twiddles; P = 64: the
+  // forward's own table, PB = 8)
   sfor<0, NR / 8>([&](auto jj) {
     constexpr int J = decltype(jj)::value;
-    dft<8, true, J * 8, 1, NR>(v);
+    sdft<8, 1, J * 8, NR>(v);
   });
   TM_STEP_FENCE();
   // step 3b': conj W_P^{a c3}
@@ -179,7 +184,8 @@ __device__ __forceinline__ void fft_inv(cf (&v)[NR], int L, const cf* twN, const
   } else {
     sfor<1, 8>([&](auto aa) {
       constexpr int A = decltype(aa)::value;
-      const cf w = twP[(A * c3) & (P - 1)];
+      constexpr float sc = (float)splan<8, 1>().sig[A];
+      const cf w = cscale(twP[(A * c3) & (P - 1)], sc);
       sfor<0, NR / 8>([&](auto jj) {
         constexpr int J = decltype(jj)::value;
         v[J * 8 + A] = cmulc(v[J * 8 + A], w);
@@ -233,8 +239,11 @@ __device__ __forceinline__ void fft_inv(cf (&v)[NR], int L, const cf* twN, const
     v[2 * K2 + 1] = cmulc(v[2 * K2 + 1], cf{t.z, t.w});
   });
   TM_STEP_FENCE();
-  // step 1': IDFT_NR over k2 -> n2
-  dft<NR, true, 0, 1, NR>(v);
+  // step 1': IDFT_NR over k2 -> n2.  The scaled twN table multiplied register
+  // k2 by splan<NR, 0>().sig[k2] on top of the twiddle, so the inputs carry
+  // 1 / that (plan 2); the outputs carry splan<NR, 2>().sig[n2], absorbed by
+  // the synthesis window (winS).
+  sdft<NR, 2, 0, NR>(v);
 }
 
 // per-lane register tables (window, gains, 1/wsum) in lane-quad layout:

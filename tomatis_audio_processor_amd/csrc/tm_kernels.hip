@@ -1229,6 +1229,7 @@ struct tomatis_plan_s {
   uint16_t* tf = nullptr;
   uint16_t* seg_start = nullptr;
   float* win = nullptr;
+  float* winS = nullptr;  // synthesis window x the register FFT's inverse output scales
   float* win2 = nullptr;
   float* winv = nullptr;
   cf* twN = nullptr;
@@ -1320,7 +1321,7 @@ const char* tomatis_status_string(int s) {
 int tomatis_plan_destroy(tomatis_plan_t p) {
   if (!p) return TOMATIS_OK;
   void* ptrs[] = {p->st, p->runs, p->lblocks, p->segs, p->seg_first, p->seg_count, p->tf,
-                  p->seg_start, p->win, p->win2, p->winv, p->twN, p->twP, p->scratch,
+                  p->seg_start, p->win, p->winS, p->win2, p->winv, p->twN, p->twP, p->scratch,
                   p->pos_base, p->chunks, p->mh_tf, p->mh_cnt, p->mh_off, p->mh_sym, p->mh_soff, p->gperm,
                   p->grp_base, p->leaf_base, p->leaves, p->gsum, p->gcarry, p->gcarry_in,
                   p->aq, p->afin, p->acin,
@@ -1548,17 +1549,26 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
     }
     p->rmax = (N + hop - 1) / hop;
     const int NRr = p->NR;
+    // scaled-DIF output scales of the register FFT (tm_common.h): the step-2
+    // table absorbs the forward NR-point DFT's, the synthesis window the
+    // inverse's (whose inputs carry 1 / the forward's)
+    const double* sigF = NRr == 32 ? splan<32, 0>().sig : splan<16, 0>().sig;
+    const double* sigI = NRr == 32 ? splan<32, 2>().sig : splan<16, 2>().sig;
     std::vector<cf> twN((size_t)NRr * P), twP(P);
     for (int k2 = 0; k2 < NRr; ++k2)
       for (int n1 = 0; n1 < P; ++n1) {
         const double ang = -2.0 * M_PI * (double)((int64_t)n1 * k2 % N) / (double)N;
-        twN[((size_t)(k2 >> 1) * P + n1) * 2 + (k2 & 1)] = {(float)cos(ang), (float)sin(ang)};
+        twN[((size_t)(k2 >> 1) * P + n1) * 2 + (k2 & 1)] = {(float)(cos(ang) * sigF[k2]),
+                                                           (float)(sin(ang) * sigF[k2])};
       }
+    std::vector<float> winS(N);
+    for (int t = 0; t < N; ++t) winS[t] = (float)((double)w[t] * sigI[t / P]);
     for (int m = 0; m < P; ++m) {
       const double ang = -2.0 * M_PI * (double)m / (double)P;
       twP[m] = {(float)cos(ang), (float)sin(ang)};
     }
     if ((rc = dalloc_copy(&p->win, w))) return rc;
+    if ((rc = dalloc_copy(&p->winS, winS))) return rc;
     if ((rc = dalloc_copy(&p->win2, w2))) return rc;
     if ((rc = dalloc_copy(&p->winv, winv))) return rc;
     if ((rc = dalloc_copy(&p->twN, twN))) return rc;
@@ -2037,6 +2047,7 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
   A.st = p->st;
   A.runs = p->runs;
   A.win = p->win;
+  A.winS = p->winS;
   A.win2 = p->win2;
   A.twN = p->twN;
   A.twP = p->twP;

@@ -37,6 +37,7 @@ struct MainArgs {
   const TomatisStream* st;
   const Run* runs;
   const float* win;     // [N]
+  const float* winS;    // [N] synthesis window x the inverse FFT's output scales (register FFT)
   const float* win2;    // [N] win*win (f32)
   const cf* twN;        // [32][P]
   const cf* twP;        // [P]

@@ -194,6 +194,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   __shared__ __attribute__((aligned(16))) cf s_twN[NR * P];
   __shared__ __attribute__((aligned(16))) cf s_twP[LT ? 8 * P : P];
   __shared__ __attribute__((aligned(16))) float s_win[N];      // lane-quad layout
+  __shared__ __attribute__((aligned(16))) float s_winS[N];     // synthesis, scaled
   __shared__ __attribute__((aligned(16))) float s_winv[SHQ * P];  // lane-quad layout
   __shared__ cf s_buf[NSEQ][G::BUF];
   __shared__ __attribute__((aligned(16))) float s_gain[GM ? 2 * N : 4];
@@ -201,7 +202,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   if constexpr (LT) {  // [m/2][l][m&1] = W_P^{(l%8)*m}
     for (int i = threadIdx.x; i < 8 * P; i += WG) {
       const int m = 2 * (i / (2 * P)) + (i & 1), l = (i / 2) % P;
-      s_twP[i] = A.twP[((l & 7) * m) & (P - 1)];
+      s_twP[i] = cscale(A.twP[((l & 7) * m) & (P - 1)], sig_at<8>(m));
     }
   } else {
     for (int i = threadIdx.x; i < P; i += WG) s_twP[i] = A.twP[i];
@@ -209,6 +210,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   for (int e = threadIdx.x; e < N; e += WG) {  // e = lq(i, l)
     const int q = e >> 2, l = q % P, i = (q / P) * 4 + (e & 3);
     s_win[e] = A.win[l + P * i];
+    s_winS[e] = A.winS[l + P * i];
   }
   for (int e = threadIdx.x; e < SHQ * P; e += WG) {
     const int q = e >> 2, l = q % P, i = (q / P) * 4 + (e & 3);
@@ -223,6 +225,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   }
   __syncthreads();
   const float4* const w4 = reinterpret_cast<const float4*>(s_win);
+  const float4* const ws4 = reinterpret_cast<const float4*>(s_winS);
 #ifdef TM_PROFILE
   const unsigned long long t_k1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -324,10 +327,10 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       TPROF(3, v[NR - 1].x);
       fft_inv<P, NR, LT>(v, L, s_twN, s_twP, buf);
       TPROF(4, v[NR - 1].x);
-      // ---- synthesis window fused with the register OLA ----
+      // ---- synthesis window (x the inverse FFT's output scales) + register OLA ----
   #pragma unroll
       for (int n4 = 0; n4 < NR / 4; ++n4) {
-        const float4 w = w4[n4 * P + L];
+        const float4 w = ws4[n4 * P + L];
         const float ww[4] = {w.x, w.y, w.z, w.w};
   #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -615,10 +618,14 @@ __global__ __launch_bounds__(256, 2) void k_stft_frames(MainArgs A) {
   __shared__ __attribute__((aligned(16))) cf s_twN[NR * P];
   __shared__ cf s_twP[P];
   __shared__ float s_win[N];
+  __shared__ float s_winS[N];
   __shared__ cf s_buf[NSEQ][G::BUF];
   for (int i = threadIdx.x; i < NR * P; i += 256) s_twN[i] = A.twN[i];
   for (int i = threadIdx.x; i < P; i += 256) s_twP[i] = A.twP[i];
-  for (int i = threadIdx.x; i < N; i += 256) s_win[i] = A.win[i];
+  for (int i = threadIdx.x; i < N; i += 256) {
+    s_win[i] = A.win[i];
+    s_winS[i] = A.winS[i];
+  }
   __syncthreads();
   const int seq = threadIdx.x / P, L = threadIdx.x % P;
   const int run_id = blockIdx.x * NSEQ + seq;
@@ -666,7 +673,7 @@ __global__ __launch_bounds__(256, 2) void k_stft_frames(MainArgs A) {
     if (live) {
       cf* dst = A.scratch + (S.frame_base + k) * (int64_t)N;
 #pragma unroll
-      for (int n2 = 0; n2 < NR; ++n2) dst[L + P * n2] = cscale(v[n2], s_win[L + P * n2]);
+      for (int n2 = 0; n2 < NR; ++n2) dst[L + P * n2] = cscale(v[n2], s_winS[L + P * n2]);
     }
   }
 }
@@ -683,7 +690,8 @@ __global__ void k_gain_perm(const float* __restrict__ g, int n_rows, int n_bins,
   const int q = e >> 2, L = q % P, i = (q / P) * 4 + (e & 3);
   int b = fft_bin<P, NR>(L, i);
   b = (b <= N / 2) ? b : N - b;
-  out[t] = g[(int64_t)row * n_bins + b] * (1.0f / (float)N);
+  // x the forward FFT's output scale of register i (its step-3c DFT_8 output)
+  out[t] = (g[(int64_t)row * n_bins + b] * (1.0f / (float)N)) * sig_at<8>(i & 7);
 }
 
 // generic-hop OLA gather: one thread per output position (frame order preserved)
@@ -832,13 +840,20 @@ __global__ __launch_bounds__(256) void k_ola_gather_lds(LdsArgs A) {
 
 template <int P, int NR, int SH, bool PF, bool NT, int WG>
 void launch_main_pf(const MainArgs& A, int ch, hipStream_t s) {
-  const int gm = A.n_rows_lds > 0 ? (A.lds_mixed ? 2 : 1) : 0;
+  // n_fft 4096 keeps its gain rows in L2: two LDS windows (analysis, scaled
+  // synthesis) + 4 sequences' exchange rows leave no room for 32 KB of gains
+  // (per-frame gain reads measured off the critical path, C3)
+  constexpr bool kNoLdsGains = P == 128 && NR == 32;
+  const int gm = kNoLdsGains ? 0 : (A.n_rows_lds > 0 ? (A.lds_mixed ? 2 : 1) : 0);
   const dim3 g((A.n_runs + WG / P - 1) / (WG / P)), b(WG);
 #ifdef TM_DEV_ONE_KERNEL  // asm studies: one instantiation (stereo, LDS gains, WG 256)
   if constexpr (WG == 256) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 1, PF, NT, WG>), g, b, 0, s, A);
   return;
 #endif
-  if (ch == 2) {
+  if constexpr (kNoLdsGains) {
+    if (ch == 2) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 0, PF, NT, WG>), g, b, 0, s, A);
+    else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, 0, PF, NT, WG>), g, b, 0, s, A);
+  } else if (ch == 2) {
     if (gm == 1) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 1, PF, NT, WG>), g, b, 0, s, A);
     else if (gm == 2) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 2, PF, NT, WG>), g, b, 0, s, A);
     else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 0, PF, NT, WG>), g, b, 0, s, A);
