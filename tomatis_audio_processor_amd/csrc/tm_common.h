@@ -362,6 +362,12 @@ __device__ __forceinline__ int opaque(int v) {
   return r;
 }
 
+__device__ __forceinline__ float opaque_f(float v) {
+  float r;
+  __asm__ volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(v));
+  return r;
+}
+
 __device__ __forceinline__ float wave_max(float v) {
   for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
   return v;

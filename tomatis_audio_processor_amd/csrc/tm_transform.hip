@@ -16,6 +16,10 @@
 using namespace tdsp;
 using namespace tshared;
 
+#ifndef TM_DEV_WG
+#define TM_DEV_WG 256
+#endif
+
 namespace {
 #ifdef TM_PROFILE  // diagnostic builds: per-phase wave cycles of the interior loop
 #define TPROF(i, dep)                                              \
@@ -226,6 +230,45 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   __syncthreads();
   const float4* const w4 = reinterpret_cast<const float4*>(s_win);
   const float4* const ws4 = reinterpret_cast<const float4*>(s_winS);
+  // register-resident per-lane tables (TM_WREG: analysis window, the synthesis
+  // window derived with the inverse's compile-time output scales; TM_TPREG:
+  // step-3b twiddles): LDS reads are the kernel's bottleneck, VGPRs are not
+  constexpr bool kTR = LT
+#ifdef TM_TPREG
+      ;
+#else
+      && false;
+#endif
+  cf tp[8];
+  tp[0] = cf{1.f, 0.f};
+  if constexpr (kTR) {
+#pragma unroll
+    for (int m = 1; m < 8; ++m)
+      tp[m] = cscale(A.twP[((threadIdx.x % P & 7) * m) & (P - 1)], sig_at<8>(m));
+  }
+#ifdef TM_TNREG
+  static_assert(P == 64 && NR == 32, "register step-2 bases: n_fft 2048");
+  constexpr bool kTN = LT;
+  cf tb[12];
+  {
+    const int l = threadIdx.x % P;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+      const int e = j < 8 ? l * j : l * 8 * (j - 8);  // exponent of W_N
+      double sn, cs;
+      sincos(-2.0 * 3.14159265358979323846 * (double)(e % N) / (double)N, &sn, &cs);
+      tb[j] = cf{(float)cs, (float)sn};
+    }
+  }
+#else
+  constexpr bool kTN = false;
+  cf tb[12];
+#endif
+#ifdef TM_WREG
+  float wr[NR];
+#pragma unroll
+  for (int i = 0; i < NR; ++i) wr[i] = A.win[threadIdx.x % P + P * i];
+#endif
 #ifdef TM_PROFILE
   const unsigned long long t_k1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -288,16 +331,21 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   #pragma unroll
         for (int n2 = 0; n2 < NR; ++n2) v[n2] = cscale(v[n2], iscale);
       }
+#ifdef TM_WREG
+  #pragma unroll
+      for (int i = 0; i < NR; ++i) v[i] = cscale(v[i], wr[i]);
+#else
   #pragma unroll
       for (int n4 = 0; n4 < NR / 4; ++n4) {
-        const float4 w = w4[n4 * P + L];
+        const float4 w = w4[TM_TIN(n4 * P + L)];
         v[4 * n4] = cscale(v[4 * n4], w.x);
         v[4 * n4 + 1] = cscale(v[4 * n4 + 1], w.y);
         v[4 * n4 + 2] = cscale(v[4 * n4 + 2], w.z);
         v[4 * n4 + 3] = cscale(v[4 * n4 + 3], w.w);
       }
+#endif
       TPROF(1, v[NR - 1].x);
-      fft_fwd<P, NR, LT>(v, L, s_twN, s_twP, buf);
+      fft_fwd<P, NR, LT, kTR, kTN>(v, L, s_twN, s_twP, buf, tp, tb);
       TPROF(2, v[NR - 1].x);
       // ---- gain row (real, even, 1/N folded in), per-lane layout ----
       bool g_lds = GM == 1;
@@ -307,7 +355,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
             reinterpret_cast<const float4*>(s_gain + ((GM == 1 ? row : row == A.lds_row[1]) ? N : 0));
   #pragma unroll
         for (int n4 = 0; n4 < NR / 4; ++n4) {
-          const float4 g = g4[n4 * P + L];
+          const float4 g = g4[TM_TIG(n4 * P + L)];
           v[4 * n4] = cscale(v[4 * n4], g.x);
           v[4 * n4 + 1] = cscale(v[4 * n4 + 1], g.y);
           v[4 * n4 + 2] = cscale(v[4 * n4 + 2], g.z);
@@ -325,13 +373,22 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
         }
       }
       TPROF(3, v[NR - 1].x);
-      fft_inv<P, NR, LT>(v, L, s_twN, s_twP, buf);
+      fft_inv<P, NR, LT, kTR, kTN>(v, L, s_twN, s_twP, buf, tp, tb);
       TPROF(4, v[NR - 1].x);
       // ---- synthesis window (x the inverse FFT's output scales) + register OLA ----
   #pragma unroll
       for (int n4 = 0; n4 < NR / 4; ++n4) {
-        const float4 w = ws4[n4 * P + L];
+#ifdef TM_WREG
+        // unscaled step 1' (TM_TNREG): the plain window
+        constexpr bool kU = kTN;
+        const float ww[4] = {kU ? wr[4 * n4] : wr[4 * n4] * (float)splan<NR, 2>().sig[4 * n4],
+                             kU ? wr[4 * n4 + 1] : wr[4 * n4 + 1] * (float)splan<NR, 2>().sig[4 * n4 + 1],
+                             kU ? wr[4 * n4 + 2] : wr[4 * n4 + 2] * (float)splan<NR, 2>().sig[4 * n4 + 2],
+                             kU ? wr[4 * n4 + 3] : wr[4 * n4 + 3] * (float)splan<NR, 2>().sig[4 * n4 + 3]};
+#else
+        const float4 w = ws4[TM_TINS(n4 * P + L)];
         const float ww[4] = {w.x, w.y, w.z, w.w};
+#endif
   #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int i = 4 * n4 + u;
@@ -348,7 +405,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
     float wv[SHQ];
 #pragma unroll
     for (int q = 0; q < SHQ / 4; ++q) {
-      const float4 t = reinterpret_cast<const float4*>(s_winv)[q * P + L];
+      const float4 t = reinterpret_cast<const float4*>(s_winv)[TM_TIG(q * P + L)];
       wv[4 * q] = t.x;
       wv[4 * q + 1] = t.y;
       wv[4 * q + 2] = t.z;
@@ -427,24 +484,39 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
 #pragma unroll
       for (int i = 0; i < SH; ++i) o[i] = cf{0.f, 0.f};
       store_out(o, rnull, 0);
+#ifndef TM_NH_DIRECT
       ld_new(min(1, nit - 1), nh);
+#endif
     }
     for (int it = 0; it < nit; ++it) {
       const uint32_t row = row_of(rw_nx, it);
       rw_nx = row_word(min(it + 1, nit - 1));
-      TPROF(0, v[0].x);
-      transform(v, row);
-      TPROF(5, v[NR - 1].x);
       const bool emit = it >= nwarm;
+      // a frame that starts a new chunk flushes the previous chunk's peak first
+      // (pk holds frames < k only).  TM_FLUSH_TOP: before the transform, where
+      // few registers are live (after it, the sunk tail of the inverse FFT stays
+      // live across both paths of the branch: peak pressure 252 -> 179 VGPRs)
+#ifdef TM_FLUSH_TOP
       if (emit && kfirst + it == next_chunk_k) {
         flush_peak<P>(pk, cid, S, A.peaks, L, done);
         ++cid;
         next_chunk_k = (cid < S.n_chunks - 1) ? next_chunk_k + chunk_k_step : INT64_MAX;
       }
+#endif
+      TPROF(0, v[0].x);
+      transform(v, row);
+      TPROF(5, v[NR - 1].x);
+#ifndef TM_FLUSH_TOP
+      if (emit && kfirst + it == next_chunk_k) {
+        flush_peak<P>(pk, cid, S, A.peaks, L, done);
+        ++cid;
+        next_chunk_k = (cid < S.n_chunks - 1) ? next_chunk_k + chunk_k_step : INT64_MAX;
+      }
+#endif
       // outputs of this frame's first hop: interior 1/sum w^2, output scale, peak
 #pragma unroll
       for (int q = 0; q < SHQ / 4; ++q) {
-        const float4 t4 = reinterpret_cast<const float4*>(s_winv)[q * P + L];
+        const float4 t4 = reinterpret_cast<const float4*>(s_winv)[TM_TIG(q * P + L)];
         wv[4 * q] = t4.x;
         wv[4 * q + 1] = t4.y;
         wv[4 * q + 2] = t4.z;
@@ -461,19 +533,35 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       for (int i = 0; i < NC; ++i) acc[i] = v[i + SH];
       // next frame's input (clamped), then this frame's stores, then the new hop
       // of the frame after next
-#if defined(TM_EXP_L1LOAD)  // timing experiments: inputs from one L1-resident frame
+#if defined(TM_EXP_NO_OLD)  // timing experiments: no reload of the overlap (wrong results)
+#elif defined(TM_EXP_L1LOAD)  // timing experiments: inputs from one L1-resident frame
       ld_old(0, v);
 #else
       ld_old(min(it + 1, nit - 1), v);
 #endif
+#if defined(TM_NH_DIRECT)  // the next frame's new hop straight from HBM (no prefetch registers)
+      {
+        cf t[SH];
+        ld_new(min(it + 1, nit - 1), t);
 #pragma unroll
-      for (int j = 0; j < SH; ++j) v[NO + j] = nh[j];
-#if defined(TM_EXP_NOSTORE)  // timing experiments: outputs dropped
+        for (int j = 0; j < SH; ++j) v[NO + j] = t[j];
+      }
+#else
+      // the arrived new hop moves into the frame here, through opaque copies: a
+      // plain assignment lets the loop-carried copy land after the next
+      // prefetch's issue, where it waits for that HBM load
+#pragma unroll
+      for (int j = 0; j < SH; ++j) v[NO + j] = cf{opaque_f(nh[j].x), opaque_f(nh[j].y)};
+#endif
+#if defined(TM_EXP_NO_ST)  // timing experiments: no output stores (wrong results)
+      if (it == 0x7fffffff) store_out(o, rnull, 0);
+#elif defined(TM_EXP_NOSTORE)  // timing experiments: outputs dropped
       store_out(o, rnull, 0);
 #else
       store_out(o, emit ? ry : rnull, emit ? (it - nwarm) * (HOP * CH * 4) : 0);
 #endif
-#if defined(TM_EXP_L1LOAD)
+#if defined(TM_EXP_NO_NEW) || defined(TM_NH_DIRECT)  // (TM_EXP_NO_NEW: wrong results)
+#elif defined(TM_EXP_L1LOAD)
       ld_new(0, nh);
 #else
       ld_new(min(it + 2, nit - 1), nh);
@@ -846,10 +934,11 @@ void launch_main_pf(const MainArgs& A, int ch, hipStream_t s) {
   constexpr bool kNoLdsGains = P == 128 && NR == 32;
   const int gm = kNoLdsGains ? 0 : (A.n_rows_lds > 0 ? (A.lds_mixed ? 2 : 1) : 0);
   const dim3 g((A.n_runs + WG / P - 1) / (WG / P)), b(WG);
-#ifdef TM_DEV_ONE_KERNEL  // asm studies: one instantiation (stereo, LDS gains, WG 256)
-  if constexpr (WG == 256) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 1, PF, NT, WG>), g, b, 0, s, A);
-  return;
-#endif
+#ifdef TM_DEV_ONE_KERNEL  // dev/asm studies: one instantiation (stereo, LDS gains)
+  (void)gm;
+  (void)ch;
+  hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 1, PF, NT, WG>), g, b, 0, s, A);
+#else
   if constexpr (kNoLdsGains) {
     if (ch == 2) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 0, PF, NT, WG>), g, b, 0, s, A);
     else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, 0, PF, NT, WG>), g, b, 0, s, A);
@@ -862,6 +951,7 @@ void launch_main_pf(const MainArgs& A, int ch, hipStream_t s) {
     else if (gm == 2) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, 2, PF, NT, WG>), g, b, 0, s, A);
     else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, 0, PF, NT, WG>), g, b, 0, s, A);
   }
+#endif
 }
 template <int P, int NR, int SH>
 void launch_main(const MainArgs& A, int ch, int wg, hipStream_t s) {
@@ -874,6 +964,10 @@ void launch_main(const MainArgs& A, int ch, int wg, hipStream_t s) {
   // P = 64: the interior loop pipelines its own input; PF only affects the
   // generic edge loop, where it stays off (register-bound).
   constexpr bool PF = NR == 16;
+#ifdef TM_DEV_ONE_KERNEL
+  (void)wg;
+  return launch_main_pf<P, NR, SH, false, true, TM_DEV_WG>(A, ch, s);
+#endif
   if constexpr (P == 64) {
     if (wg == 512) return launch_main_pf<P, NR, SH, false, true, 512>(A, ch, s);
     return launch_main_pf<P, NR, SH, false, true, 256>(A, ch, s);
@@ -893,6 +987,10 @@ void launch_main(const MainArgs& A, int ch, int wg, hipStream_t s) {
 namespace tshared {
 
 int transform_wg(int P, int NR) {
+#ifdef TM_DEV_ONE_KERNEL
+  (void)P, (void)NR;
+  return TM_DEV_WG;
+#endif
   // P = 64 (n_fft 2048): the interior loop needs ~250 VGPRs (2 waves/SIMD), so
   // two 4-sequence blocks per CU (TOMATIS_WG=512: one 8-sequence block, the
   // same occupancy with one copy of the tables; measured equal).
@@ -914,8 +1012,7 @@ int transform_slots_per_cu(int P, int NR) {
 void launch_transform(const MainArgs& A, int P, int NR, int SH, int ch, int wg, hipStream_t s) {
 #ifdef TM_DEV_ONLY_2048_512  // development builds: the headline configuration only
   if (P == 64 && SH == 8) launch_main<64, 32, 8>(A, ch, wg, s);
-  return;
-#endif
+#else
   if (P == 64) {
     if (SH == 4) launch_main<64, 32, 4>(A, ch, wg, s);
     else if (SH == 8) launch_main<64, 32, 8>(A, ch, wg, s);
@@ -929,15 +1026,17 @@ void launch_transform(const MainArgs& A, int P, int NR, int SH, int ch, int wg, 
     else if (SH == 8) launch_main<128, 32, 8>(A, ch, wg, s);
     else launch_main<128, 32, 16>(A, ch, wg, s);
   }
+#endif
 }
 
 void launch_frames(const MainArgs& A, int P, int NR, int blocks, hipStream_t s) {
 #ifdef TM_DEV_ONE_KERNEL
-  return;
-#endif
+  (void)A, (void)P, (void)NR, (void)blocks, (void)s;
+#else
   if (P == 64) hipLaunchKernelGGL((k_stft_frames<64, 32>), dim3(blocks), dim3(256), 0, s, A);
   else if (NR == 16) hipLaunchKernelGGL((k_stft_frames<128, 16>), dim3(blocks), dim3(256), 0, s, A);
   else hipLaunchKernelGGL((k_stft_frames<128, 32>), dim3(blocks), dim3(256), 0, s, A);
+#endif
 }
 
 void launch_gain_perm(int P, int NR, const float* gains, int n_rows, int n_bins, float* out,
@@ -956,7 +1055,9 @@ void launch_lds_frames(const LdsArgs& A, hipStream_t s) {
   const dim3 g((unsigned)A.total_frames, (unsigned)((A.ch + 1) / 2));
 #define LDS_N(NN) \
   if (A.n_fft == NN) hipLaunchKernelGGL((k_stft_lds<NN>), g, dim3(256), 0, s, A);
+#ifndef TM_DEV_ONE_KERNEL
   LDS_N(256) LDS_N(512) LDS_N(1024) LDS_N(2048) LDS_N(4096) LDS_N(8192)
+#endif
 #undef LDS_N
 }
 

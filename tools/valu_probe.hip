@@ -8,7 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
-template <int KIND>  // 0 v_fma_f32, 1 v_pk_fma_f32, 2 v_add_f32, 3 v_pk_add_f32
+template <int KIND>  // 0 v_fma_f32, 1 v_pk_fma_f32, 2 v_add_f32, 3 v_pk_add_f32,
+                    // 4 v_mul_f32, 5 v_pk_mul_f32, 6 v_fmac_f32 with a literal, 7 v_fma_f32 SGPR operand
 __global__ __launch_bounds__(1024) void k_probe(float* out, int iters, unsigned long long* cyc) {
   typedef float f2 __attribute__((ext_vector_type(2)));
   f2 a[8];
@@ -32,8 +33,25 @@ __global__ __launch_bounds__(1024) void k_probe(float* out, int iters, unsigned 
         __asm__ volatile("v_add_f32 %0, %0, %1" : "+v"(x) : "v"(c.x));
         __asm__ volatile("v_add_f32 %0, %0, %1" : "+v"(y) : "v"(c.y));
         a[u] = f2{x, y};
-      } else {
+      } else if constexpr (KIND == 3) {
         __asm__ volatile("v_pk_add_f32 %0, %0, %1" : "+v"(a[u]) : "v"(c));
+      } else if constexpr (KIND == 4) {
+        float x = a[u].x, y = a[u].y;
+        __asm__ volatile("v_mul_f32 %0, %0, %1" : "+v"(x) : "v"(b.x));
+        __asm__ volatile("v_mul_f32 %0, %0, %1" : "+v"(y) : "v"(b.y));
+        a[u] = f2{x, y};
+      } else if constexpr (KIND == 5) {
+        __asm__ volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(a[u]) : "v"(b));
+      } else if constexpr (KIND == 6) {
+        float x = a[u].x, y = a[u].y;
+        __asm__ volatile("v_fmac_f32 %0, 0x3f7fbe77, %1" : "+v"(x) : "v"(c.x));
+        __asm__ volatile("v_fmac_f32 %0, 0x3f7fbe77, %1" : "+v"(y) : "v"(c.y));
+        a[u] = f2{x, y};
+      } else {
+        float x = a[u].x, y = a[u].y;
+        __asm__ volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(x) : "s"(b.x), "v"(c.x));
+        __asm__ volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(y) : "s"(b.y), "v"(c.y));
+        a[u] = f2{x, y};
       }
     }
   }
@@ -48,7 +66,7 @@ __global__ __launch_bounds__(1024) void k_probe(float* out, int iters, unsigned 
 template <int KIND>
 void run(const char* name, int ncu, float* out, unsigned long long* cyc) {
   const int iters = 4096;
-  const int instr_per_iter = (KIND == 1 || KIND == 3) ? 8 : 16;
+  const int instr_per_iter = (KIND == 1 || KIND == 3 || KIND == 5) ? 8 : 16;
   for (int w = 1; w <= 4; ++w) {
     double cpw = 0;
     for (int pass = 0; pass < 2; ++pass) {
@@ -78,5 +96,9 @@ int main() {
   run<1>("v_pk_fma_f32", ncu, out, cyc);
   run<2>("v_add_f32", ncu, out, cyc);
   run<3>("v_pk_add_f32", ncu, out, cyc);
+  run<4>("v_mul_f32", ncu, out, cyc);
+  run<5>("v_pk_mul_f32", ncu, out, cyc);
+  run<6>("v_fmac_f32 lit", ncu, out, cyc);
+  run<7>("v_fma_f32 sgpr", ncu, out, cyc);
   return 0;
 }
