@@ -76,6 +76,9 @@ struct FftGeo {
   static constexpr int RW = P + 8;          // LDS row stride (complex)
   static constexpr int ROUNDS = NR / PB;    // exchange rounds
   static constexpr int BUF = PB * RW;       // complex per round buffer
+  // LDS per sequence: the round buffer, then (P > 64) one slot holding the
+  // pair-barrier counter of the sequence's two waves
+  static constexpr int SEQ_LDS = BUF + (P > 64 ? 1 : 0);
   static_assert(PB >= 4 && PB <= NR && NR % 8 == 0, "need 4 <= P/8 <= NR, NR % 8 == 0");
 };
 
@@ -83,11 +86,40 @@ struct FftGeo {
 __device__ inline constexpr cf kNoTp[8] = {};
 __device__ inline constexpr cf kNoTb[12] = {};
 
-// LDS synchronisation for an exchange: wave-local when P == 64.
-template <int P>
-__device__ __forceinline__ void xsync() {
+// Barrier of the two waves of a P = 128 sequence (not the whole workgroup):
+// a counter in the sequence's LDS slot.  Both waves add 1 per barrier and can
+// be at most one barrier apart, so the old value o of barrier k is 2k or
+// 2k + 1 and the barrier completes when the counter reaches 2k + 2.  LDS
+// operations of a wave execute in order, so the writes before the add are
+// visible to the partner's reads after its poll.  Bounded spin: a stuck
+// partner sets the error flag instead of hanging the GPU.
+__device__ __forceinline__ void pair_barrier(uint32_t* ctr, uint32_t* err) {
+  uint32_t o = 0;
+  if ((threadIdx.x & 63) == 0)
+    o = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  o = __builtin_amdgcn_readfirstlane(o);
+  const uint32_t target = (o & ~1u) + 2u;
+  for (int spin = 0; spin < (1 << 22); ++spin) {
+    const uint32_t c = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+    if ((int32_t)(c - target) >= 0) return;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  if (err && (threadIdx.x & 63) == 0) atomicOr(err, 2u);
+}
+
+// LDS synchronisation for an exchange: wave-local when P == 64, the pair
+// barrier when P == 128 (counter at buf[BUF]), else the workgroup barrier.
+template <int P, int NR = 32>
+__device__ __forceinline__ void xsync(cf* buf = nullptr, uint32_t* err = nullptr) {
 #ifdef TM_EXP_NOSYNC  // timing experiments only (wrong results): no exchange ordering
   if constexpr (P <= 64) return;
+#endif
+#ifndef TM_NO_PAIRSYNC
+  if constexpr (P == 128) {
+    pair_barrier(reinterpret_cast<uint32_t*>(buf + FftGeo<P, NR>::BUF), err);
+    return;
+  }
 #endif
   if constexpr (P <= 64) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -110,7 +142,7 @@ __device__ __forceinline__ int x2col(int a, int c) { return 8 * c + (a ^ (c & 7)
 template <int P, int NR = 32, bool LT = false, bool TR = false, bool TN = false>
 __device__ __forceinline__ void fft_fwd(cf (&v)[NR], int L, const cf* twN, const cf* twP,
                                         cf* buf, const cf (&tp)[8] = kNoTp,
-                                        const cf (&tb)[12] = kNoTb) {
+                                        const cf (&tb)[12] = kNoTb, uint32_t* err = nullptr) {
   using G = FftGeo<P, NR>;
   constexpr int PB = G::PB, RW = G::RW;
   const int a1 = L & 7, q1 = L >> 3;
@@ -129,7 +161,9 @@ __device__ __forceinline__ void fft_fwd(cf (&v)[NR], int L, const cf* twN, const
     });
   } else {
   // step 1 (outputs carry splan<NR, 0>().sig: the twN table absorbs them)
+#ifndef TM_EXP_SKIP1F  // timing experiments only (wrong results): no step-1 DFT
   sdft<NR, 0, 0, NR>(v);
+#endif
   TM_STEP_FENCE();
   // step 2 (twiddles in lane-pair layout: one ds_read_b128 per two registers)
   sfor<0, NR / 2>([&](auto kk) {
@@ -146,12 +180,12 @@ __device__ __forceinline__ void fft_fwd(cf (&v)[NR], int L, const cf* twN, const
       constexpr int K = decltype(kk)::value;
       buf[K * RW + L] = v[R * PB + K];
     });
-    xsync<P>();
+    xsync<P, NR>(buf, err);
     sfor<0, PB>([&](auto bb) {
       constexpr int B = decltype(bb)::value;
       v[R * PB + B] = buf[q1 * RW + a1 + 8 * B];
     });
-    xsync<P>();
+    xsync<P, NR>(buf, err);
   });
   TM_STEP_FENCE();
   // step 3a: DFT_PB over b for each j (output c carries splan<PB, 0>().sig[c],
@@ -200,7 +234,7 @@ __device__ __forceinline__ void fft_fwd(cf (&v)[NR], int L, const cf* twN, const
       constexpr int C = decltype(cc)::value;
       buf[q1 * RW + x2col(a1, C)] = v[R * PB + C];
     });
-    xsync<P>();
+    xsync<P, NR>(buf, err);
     sfor<0, PB / 8>([&](auto jj) {
       constexpr int JJ = decltype(jj)::value;
       const int row = q3 + 8 * JJ;
@@ -209,7 +243,7 @@ __device__ __forceinline__ void fft_fwd(cf (&v)[NR], int L, const cf* twN, const
         v[R * PB + JJ * 8 + A] = buf[row * RW + x2col(A, c3)];
       });
     });
-    xsync<P>();
+    xsync<P, NR>(buf, err);
   });
   TM_STEP_FENCE();
   // step 3c: DFT_8 over a (output d carries splan<8, 0>().sig[d], absorbed by
@@ -224,7 +258,7 @@ __device__ __forceinline__ void fft_fwd(cf (&v)[NR], int L, const cf* twN, const
 template <int P, int NR = 32, bool LT = false, bool TR = false, bool TN = false>
 __device__ __forceinline__ void fft_inv(cf (&v)[NR], int L, const cf* twN, const cf* twP,
                                         cf* buf, const cf (&tp)[8] = kNoTp,
-                                        const cf (&tb)[12] = kNoTb) {
+                                        const cf (&tb)[12] = kNoTb, uint32_t* err = nullptr) {
   using G = FftGeo<P, NR>;
   constexpr int PB = G::PB, RW = G::RW;
   const int a1 = L & 7, q1 = L >> 3;
@@ -278,12 +312,12 @@ __device__ __forceinline__ void fft_inv(cf (&v)[NR], int L, const cf* twN, const
         buf[row * RW + x2col(A, c3)] = v[R * PB + JJ * 8 + A];
       });
     });
-    xsync<P>();
+    xsync<P, NR>(buf, err);
     sfor<0, PB>([&](auto cc) {
       constexpr int C = decltype(cc)::value;
       v[R * PB + C] = buf[q1 * RW + x2col(a1, C)];
     });
-    xsync<P>();
+    xsync<P, NR>(buf, err);
   });
   TM_STEP_FENCE();
   // step 3a': IDFT_PB over c -> b
@@ -298,12 +332,12 @@ __device__ __forceinline__ void fft_inv(cf (&v)[NR], int L, const cf* twN, const
       constexpr int B = decltype(bb)::value;
       buf[q1 * RW + a1 + 8 * B] = v[R * PB + B];
     });
-    xsync<P>();
+    xsync<P, NR>(buf, err);
     sfor<0, PB>([&](auto kk) {
       constexpr int K = decltype(kk)::value;
       v[R * PB + K] = buf[K * RW + L];
     });
-    xsync<P>();
+    xsync<P, NR>(buf, err);
   });
   TM_STEP_FENCE();
   if constexpr (TN) {
@@ -330,7 +364,9 @@ __device__ __forceinline__ void fft_inv(cf (&v)[NR], int L, const cf* twN, const
   // k2 by splan<NR, 0>().sig[k2] on top of the twiddle, so the inputs carry
   // 1 / that (plan 2); the outputs carry splan<NR, 2>().sig[n2], absorbed by
   // the synthesis window (winS).
+#ifndef TM_EXP_SKIP1I
   sdft<NR, 2, 0, NR>(v);
+#endif
 }
 
 // per-lane register tables (window, gains, 1/wsum) in lane-quad layout:

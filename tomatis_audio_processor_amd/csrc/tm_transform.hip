@@ -200,7 +200,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   __shared__ __attribute__((aligned(16))) float s_win[N];      // lane-quad layout
   __shared__ __attribute__((aligned(16))) float s_winS[N];     // synthesis, scaled
   __shared__ __attribute__((aligned(16))) float s_winv[SHQ * P];  // lane-quad layout
-  __shared__ cf s_buf[NSEQ][G::BUF];
+  __shared__ cf s_buf[NSEQ][G::SEQ_LDS];
   __shared__ __attribute__((aligned(16))) float s_gain[GM ? 2 * N : 4];
   for (int i = threadIdx.x; i < NR * P; i += WG) s_twN[i] = A.twN[i];
   if constexpr (LT) {  // [m/2][l][m&1] = W_P^{(l%8)*m}
@@ -226,6 +226,9 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   } else if constexpr (GM == 2) {
     for (int i = threadIdx.x; i < 2 * N; i += WG)
       s_gain[i] = A.gains[(int64_t)A.lds_row[i >= N] * N + (i >= N ? i - N : i)];
+  }
+  if constexpr (P > 64) {  // pair-barrier counters (tm_fft.h)
+    if (threadIdx.x < NSEQ) reinterpret_cast<uint32_t*>(s_buf[threadIdx.x] + G::BUF)[0] = 0u;
   }
   __syncthreads();
   const float4* const w4 = reinterpret_cast<const float4*>(s_win);
@@ -285,6 +288,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   const TomatisStream S = A.st[R.s];
   const int64_t kfirst = max<int64_t>(0, R.ka - (A.rmax - 1));
   int nit = valid ? (int)(R.kb - kfirst) : 0;
+#ifdef TM_NO_PAIRSYNC
   if constexpr (P > 64) {  // the block's sequences share barriers: same trip count
     __shared__ int s_nit[NSEQ];
     if (L == 0) s_nit[seq] = nit;
@@ -293,6 +297,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
     for (int i = 0; i < NSEQ; ++i) m = max(m, s_nit[i]);
     nit = m;
   }
+#endif
   cf* buf = s_buf[seq];
   const float* xs = A.x + S.in_off;
   float* ys = A.y + S.out_off;
@@ -345,7 +350,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       }
 #endif
       TPROF(1, v[NR - 1].x);
-      fft_fwd<P, NR, LT, kTR, kTN>(v, L, s_twN, s_twP, buf, tp, tb);
+      fft_fwd<P, NR, LT, kTR, kTN>(v, L, s_twN, s_twP, buf, tp, tb, A.err);
       TPROF(2, v[NR - 1].x);
       // ---- gain row (real, even, 1/N folded in), per-lane layout ----
       bool g_lds = GM == 1;
@@ -373,7 +378,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
         }
       }
       TPROF(3, v[NR - 1].x);
-      fft_inv<P, NR, LT, kTR, kTN>(v, L, s_twN, s_twP, buf, tp, tb);
+      fft_inv<P, NR, LT, kTR, kTN>(v, L, s_twN, s_twP, buf, tp, tb, A.err);
       TPROF(4, v[NR - 1].x);
       // ---- synthesis window (x the inverse FFT's output scales) + register OLA ----
   #pragma unroll
@@ -707,12 +712,15 @@ __global__ __launch_bounds__(256, 2) void k_stft_frames(MainArgs A) {
   __shared__ cf s_twP[P];
   __shared__ float s_win[N];
   __shared__ float s_winS[N];
-  __shared__ cf s_buf[NSEQ][G::BUF];
+  __shared__ cf s_buf[NSEQ][G::SEQ_LDS];
   for (int i = threadIdx.x; i < NR * P; i += 256) s_twN[i] = A.twN[i];
   for (int i = threadIdx.x; i < P; i += 256) s_twP[i] = A.twP[i];
   for (int i = threadIdx.x; i < N; i += 256) {
     s_win[i] = A.win[i];
     s_winS[i] = A.winS[i];
+  }
+  if constexpr (P > 64) {  // pair-barrier counters (tm_fft.h)
+    if (threadIdx.x < NSEQ) reinterpret_cast<uint32_t*>(s_buf[threadIdx.x] + G::BUF)[0] = 0u;
   }
   __syncthreads();
   const int seq = threadIdx.x / P, L = threadIdx.x % P;
@@ -725,6 +733,7 @@ __global__ __launch_bounds__(256, 2) void k_stft_frames(MainArgs A) {
   }
   const TomatisStream S = A.st[R.s];
   int nit = valid ? (int)(R.kb - R.ka) : 0;
+#ifdef TM_NO_PAIRSYNC
   if constexpr (P > 64) {
     __shared__ int s_nit[NSEQ];
     if (L == 0) s_nit[seq] = nit;
@@ -733,6 +742,7 @@ __global__ __launch_bounds__(256, 2) void k_stft_frames(MainArgs A) {
     for (int i = 0; i < NSEQ; ++i) m = max(m, s_nit[i]);
     nit = m;
   }
+#endif
   cf* buf = s_buf[seq];
   const float* xs = A.x + S.in_off;
   const int hop = A.hop;
@@ -752,12 +762,12 @@ __global__ __launch_bounds__(256, 2) void k_stft_frames(MainArgs A) {
       const float w = s_win[L + P * n2];
       v[n2] = {(z.x * S.in_scale) * w, (z.y * S.in_scale) * w};
     }
-    fft_fwd<P, NR>(v, L, s_twN, s_twP, buf);
+    fft_fwd<P, NR>(v, L, s_twN, s_twP, buf, kNoTp, kNoTb, A.err);
     const uint16_t row = live ? A.rows[S.frame_base + k] : 0;
     const float* g = A.gains + (int64_t)row * N;
 #pragma unroll
     for (int i = 0; i < NR; ++i) v[i] = cscale(v[i], g[lq<P>(i, L)]);
-    fft_inv<P, NR>(v, L, s_twN, s_twP, buf);
+    fft_inv<P, NR>(v, L, s_twN, s_twP, buf, kNoTp, kNoTb, A.err);
     if (live) {
       cf* dst = A.scratch + (S.frame_base + k) * (int64_t)N;
 #pragma unroll
