@@ -572,6 +572,10 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       ld_new(min(it + 2, nit - 1), nh);
 #endif
       TPROF(6, acc[0].x);
+#ifdef TM_EXP_NOPS  // diagnostic: N extra 4-byte s_nop per frame (instruction-fetch sensitivity)
+#pragma unroll
+      for (int q = 0; q < TM_EXP_NOPS; ++q) __asm__ volatile("s_nop 0");
+#endif
     }
 #ifdef TM_PROFILE
     if (L == 0) {
