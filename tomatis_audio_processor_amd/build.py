@@ -3,11 +3,9 @@
 Three translation units, compiled in parallel and linked into one C-ABI library:
 
 * ``tm_kernels.hip``   levels, gate, limiter, plan and the ``extern "C"`` entry points;
-* ``tm_transform.hip`` the fused transform kernels, compiled with the max-ILP
-  machine scheduler (``-amdgpu-sched-strategy=max-ilp``), which keeps the
-  per-frame LDS table reads batched instead of serialising them.  The other unit
-  keeps the default scheduler so the streaming kernels stay at low register
-  counts (high occupancy);
+* ``tm_transform.hip`` the fused transform kernels (FMA contraction on;
+  ``TOMATIS_TRANSFORM_SCHED`` selects another LLVM machine scheduler for
+  experiments — measured within 1 % of the default);
 * ``tm_analysis.hip``  analysis spectra for the validators / calibration tools
   (SURVEY.md §8 rows f3/f4).
 """

@@ -1,8 +1,18 @@
 // tm_transform.hip — the fused framing -> window -> FFT -> gain -> IFFT ->
 // window -> OLA -> normalise (-> limiter) kernels for gfx950, and their
-// launchers.  Own translation unit: built with the max-ILP machine scheduler,
-// which batches the per-frame LDS table reads instead of serialising them.
+// launchers.  Own translation unit (LLVM's default scheduler: max-ilp,
+// max-memory-clause and the iterative strategies measured within 1 %).
 // Reference: src/process_tomatis.py:394-406,419-426,451-453 (see tm_kernels.hip).
+//
+// Build switches (none set in the product build; DESIGN.md §6 has the numbers):
+//   development  TM_DEV_ONE_KERNEL, TM_DEV_ONLY_2048_512, TM_DEV_WG (one
+//                instantiation, 15 s builds), TM_PROFILE (per-phase cycles)
+//   alternatives TM_FLUSH_TOP, TM_NH_DIRECT (3 waves/SIMD spill-free with
+//                TM_DEV_WG=768), TM_TPREG / TM_WREG / TM_TNREG (register-
+//                resident tables), TM_VCF (packed fp32 complex, tm_common.h),
+//                TM_NO_PAIRSYNC (workgroup barriers for two-wave frames)
+//   timing only  TM_EXP_* (results are wrong on purpose: missing loads, stores,
+//                exchanges, tables or DFTs, or s_nop padding)
 #include <hip/hip_runtime.h>
 
 #include <climits>
