@@ -10,7 +10,9 @@
 //   alternatives TM_FLUSH_TOP, TM_NH_DIRECT (3 waves/SIMD spill-free with
 //                TM_DEV_WG=768), TM_TPREG / TM_WREG / TM_TNREG (register-
 //                resident tables), TM_VCF (packed fp32 complex, tm_common.h),
-//                TM_NO_PAIRSYNC (workgroup barriers for two-wave frames)
+//                TM_NO_PAIRSYNC (workgroup barriers for two-wave frames),
+//                TM_ST_CACHED / TM_LIM_CACHED (cache policy of the output and
+//                of the limiter's re-reads)
 //   timing only  TM_EXP_* (results are wrong on purpose: missing loads, stores,
 //                exchanges, tables or DFTs, or s_nop padding)
 #include <hip/hip_runtime.h>
@@ -122,7 +124,11 @@ __device__ void limit_own(const MainArgs& A, const TomatisStream& S, int gc, int
     f4v t[U];
 #pragma unroll
     for (int u = 0; u < U; ++u)
+#ifdef TM_LIM_CACHED  // experiment: limiter re-reads through the caches
+      if (i + 64 * u < n4) t[u] = b4[i + 64 * u];
+#else
       if (i + 64 * u < n4) t[u] = __builtin_nontemporal_load(b4 + i + 64 * u);
+#endif
 #pragma unroll
     for (int u = 0; u < U; ++u)
       if (i + 64 * u < n4) __builtin_nontemporal_store(t[u] * sc, b4 + i + 64 * u);
@@ -484,7 +490,11 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
     auto store_out = [&](const cf (&o)[SH], __amdgpu_buffer_rsrc_t r, int so) {
 #pragma unroll
       for (int i = 0; i < SH; ++i) {
+#ifdef TM_ST_CACHED  // experiment: output stores through the caches (limiter re-reads)
+        if constexpr (false) bstore<CH, 2>(o[i], r, L * CH * 4, so + P * i * CH * 4);
+#else
         if constexpr (NT) bstore<CH, 2>(o[i], r, L * CH * 4, so + P * i * CH * 4);
+#endif
         else bstore<CH>(o[i], r, L * CH * 4, so + P * i * CH * 4);
       }
     };
