@@ -81,12 +81,26 @@ class ChainC5:
         lin, _ = dsp.build_eq_from_residual(np.fft.rfftfreq(n_fft, 1.0 / sr), rf, res_s)
         self.s2 = engine.StaticEqPipeline(ss2, lin, n_fft=n_fft, hop=hop, pad=False)
 
-    def run(self, marks=None):
-        self.s1.run(marks=marks)
-        return self.s2.run()
+    def run(self, marks=None, check_device=True):
+        self.s1.run(marks=marks, check_device=check_device)
+        return self.s2.run(check_device=check_device)
+
+    def finish(self):
+        return self.s1.finish() | self.s2.finish()
 
     def result(self):
         return self.s1.result()
+
+
+def plans_of(pipe):
+    """Every tomatis plan a bench pipeline launches on."""
+    if isinstance(pipe, ChainC5):
+        return [pipe.s1.plan, pipe.s2.plan]
+    if hasattr(pipe, "pipes"):          # AdaptiveGroups
+        return [p.plan for p in pipe.pipes]
+    if hasattr(pipe, "rn"):             # timeshard.RankStep
+        return [pipe.rn.pipe.plan]
+    return [pipe.plan]
 
 
 def dist_init():
@@ -255,7 +269,7 @@ def main():
     torch.cuda.synchronize()
 
     for _ in range(a.warmup):
-        pipe.run()
+        pipe.run()          # device error word checked after every warm-up pass
     torch.cuda.synchronize()
     if ws > 1:
         dist.barrier()
@@ -264,17 +278,22 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(a.steps):
-        pipe.run(marks=marks[k])
+        pipe.run(marks=marks[k], check_device=False)
     torch.cuda.synchronize()
     if ws > 1:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
+    # the timed passes' device error word, read once after the timed region: a
+    # fired check (fused-limiter wait / exchange barrier) invalidates the line
+    dev_err = 0
+    for pl in plans_of(pipe):
+        dev_err |= pl.error_bits()
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in marks]))
     if ws > 1:
-        tt = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([elapsed, kern_ms, dev_err], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(tt[0]), float(tt[1])
+        elapsed, kern_ms, dev_err = float(tt[0]), float(tt[1]), int(tt[2])
 
     # per-stream manifest: (rank, stream, frames, C2 frames, max chunk peak bits)
     res = pipe.result()
@@ -330,6 +349,7 @@ def main():
                         "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                         "frac": round(tflops / FP32_PEAK_TFLOPS, 4),
                         "flop_per_ch_sample": round(flops_per_ch_sample(n_fft, hop), 1)},
+            "device_error": dev_err,
             "cpu_baseline": cpu,
             "manifest": {"streams": int(man.shape[0]),
                          "c2_fraction": round(float(man[:, 3].sum() / max(1, man[:, 2].sum())), 4)},
@@ -338,6 +358,9 @@ def main():
     if ws > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if dev_err:
+        raise SystemExit(f"device error bits {dev_err:#x} during the timed passes: "
+                         "the measurement is invalid")
 
 
 if __name__ == "__main__":

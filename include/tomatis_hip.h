@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define TOMATIS_ABI_VERSION 4
+#define TOMATIS_ABI_VERSION 5
 
 #define TOMATIS_OK 0
 #define TOMATIS_E_ARG (-1)        /* bad argument */
@@ -243,9 +243,33 @@ int tomatis_stft_ola_limited_edges(tomatis_plan_t plan, const float* x, const fl
 int tomatis_apply_limiter_edges(tomatis_plan_t plan, float* y, const uint32_t* chunk_peak_bits,
                                 float limit, int32_t edge_mask, void* hip_stream);
 
-/* Synchronous: TOMATIS_E_HIP if a device-side consistency check of the plan's
- * kernels has fired since creation (fused-limiter wait bound), else OK. */
+/* Device-side consistency checks of the plan's kernels (bits of the plan's
+ * error word):
+ *   TOMATIS_ERR_LIMITER_WAIT  a fused-limiter wave gave up waiting for its
+ *       chunk's flushes (bounded spin) and left its samples of that chunk
+ *       unscaled: the launch's output is incomplete; re-run it with
+ *       TOMATIS_OPT_FUSE_LIMITER = 0 (transform, then tomatis_apply_limiter).
+ *   TOMATIS_ERR_PAIR_BARRIER  a two-wave (n_fft 4096) exchange barrier timed
+ *       out: that launch's FFTs are wrong; no retry makes it safe.
+ * Synchronous: tomatis_plan_error returns TOMATIS_E_HIP if any bit is set
+ * since creation (or the last reset), else OK; tomatis_plan_error_bits returns
+ * the bits and clears them when reset != 0.  Replaces nothing in the
+ * reference (its loop has no asynchronous device work to check). */
+#define TOMATIS_ERR_LIMITER_WAIT 1u
+#define TOMATIS_ERR_PAIR_BARRIER 2u
 int tomatis_plan_error(tomatis_plan_t plan, void* hip_stream);
+int tomatis_plan_error_bits(tomatis_plan_t plan, uint32_t* bits, int32_t reset,
+                            void* hip_stream);
+
+/* Plan options (synchronous, host-side):
+ *   TOMATIS_OPT_FUSE_LIMITER (1 default / 0): limiter inside the transform
+ *       kernel where eligible, or always the separate tomatis_apply_limiter.
+ *   TOMATIS_OPT_LIMITER_SPIN: polls a fused-limiter wave makes before it gives
+ *       up (default 2^18; 0 forces TOMATIS_ERR_LIMITER_WAIT: fault-injection
+ *       tests of the host's recovery path). */
+#define TOMATIS_OPT_FUSE_LIMITER 1
+#define TOMATIS_OPT_LIMITER_SPIN 2
+int tomatis_plan_set_option(tomatis_plan_t plan, int32_t option, int64_t value);
 
 /* max |x| over n floats as float bits (out zeroed by caller). */
 int tomatis_absmax(const float* x, int64_t n, uint32_t* out_bits, void* hip_stream);

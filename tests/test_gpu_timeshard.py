@@ -63,3 +63,61 @@ def test_timeshard_vs_oracle(secs, sr, n_fft, hop, world):
         assert err.max() <= 1e-4
         if c < len(b) - 2:   # interior chunks: no ill-conditioned sample in them
             assert abs(gs / rs - 1) <= 5e-5
+
+
+def _rank_worker(rank, ws, port, secs, sr, q):
+    """One rank of a real 2-process run: RankStep.run with its device-resident
+    collectives (int32 gate-summary all_gather, chunk-peak all_reduce MAX) over
+    gloo on CUDA tensors (two ranks share the box's one GPU, which RCCL does
+    not allow)."""
+    import os
+    import torch
+    import torch.distributed as dist
+    from tomatis_audio_processor_amd import timeshard as T
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        N = sr * secs + 123
+        x = synth_stream(31, N, 2, sr)
+        sh = T.plan_shards(N, 2048, 512, ws)[rank]
+        xs = torch.from_numpy(x[sh.lo:sh.hi].reshape(-1).copy()).cuda()
+        step = T.RankStep(xs, sr, N, rank, ws, ch=2, gate_ui=50, n_fft=2048, hop=512)
+        res = step.run()
+        torch.cuda.synchronize()
+        st = res.stream_states(0)[sh.k0 - sh.b:sh.k1 - sh.b]
+        q.put((rank, res.output(0).copy(), st.copy(), res.stream_peaks(0).copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rankstep_two_processes_gloo():
+    """RankStep.run in 2 real ranks: concatenated outputs and
+    states equal run_emulated's, which equals the unsharded run."""
+    torch, E, T = _engine()
+    import socket
+    import torch.multiprocessing as mp
+    secs, sr, ws = 150, 44100, 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_worker, args=(r, ws, port, secs, sr, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    try:
+        out = sorted([q.get(timeout=240) for _ in range(ws)], key=lambda t: t[0])
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    N = sr * secs + 123
+    x = synth_stream(31, N, 2, sr)
+    y_em, st_em, pk_em = T.run_emulated(x, sr, ws, gate_ui=50, n_fft=2048, hop=512)
+    y = np.concatenate([o[1] for o in out])
+    st = np.concatenate([o[2] for o in out])
+    assert y.tobytes() == y_em.tobytes()
+    assert np.array_equal(st, st_em)

@@ -31,9 +31,23 @@ def test_library_exports_all_symbols():
     missing = [n for n in declared() if not hasattr(h, n)]
     assert not missing, missing
     assert set(_lib.EXPORTS) == set(declared())
-    assert h.tomatis_abi_version() == 4
+    assert h.tomatis_abi_version() == _lib.ABI_VERSION == 5
     h.tomatis_status_string.restype = ctypes.c_char_p
     assert h.tomatis_status_string(-2).decode().startswith("configuration")
+
+
+def test_header_constants_match_binding():
+    from tomatis_audio_processor_amd import _lib
+    src = open(HEADER).read()
+    defs = dict(re.findall(r"#define (TOMATIS_[A-Z0-9_]+) \(?(-?\d+)u?\)?", src))
+    for name, val in [("TOMATIS_ABI_VERSION", _lib.ABI_VERSION),
+                      ("TOMATIS_GATE_SEGMENT", _lib.GATE_SEGMENT),
+                      ("TOMATIS_GATE_NONE", _lib.GATE_NONE),
+                      ("TOMATIS_ERR_LIMITER_WAIT", _lib.ERR_LIMITER_WAIT),
+                      ("TOMATIS_ERR_PAIR_BARRIER", _lib.ERR_PAIR_BARRIER),
+                      ("TOMATIS_OPT_FUSE_LIMITER", _lib.OPT_FUSE_LIMITER),
+                      ("TOMATIS_OPT_LIMITER_SPIN", _lib.OPT_LIMITER_SPIN)]:
+        assert int(defs[name]) == val, name
 
 
 def test_struct_layout_matches_header():

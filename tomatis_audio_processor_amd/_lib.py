@@ -14,9 +14,13 @@ import ctypes as C
 import os
 
 LIB_NAME = "libtomatis_hip.so"
-ABI_VERSION = 4  # include/tomatis_hip.h TOMATIS_ABI_VERSION
+ABI_VERSION = 5  # include/tomatis_hip.h TOMATIS_ABI_VERSION
 GATE_SEGMENT = 1024      # TOMATIS_GATE_SEGMENT
 GATE_NONE = -536870912   # TOMATIS_GATE_NONE
+ERR_LIMITER_WAIT = 1     # TOMATIS_ERR_LIMITER_WAIT
+ERR_PAIR_BARRIER = 2     # TOMATIS_ERR_PAIR_BARRIER
+OPT_FUSE_LIMITER = 1     # TOMATIS_OPT_FUSE_LIMITER
+OPT_LIMITER_SPIN = 2     # TOMATIS_OPT_LIMITER_SPIN
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 F32, F64 = 0, 1
@@ -90,6 +94,8 @@ _SIGS = {
     "tomatis_ts_summary": (C.c_int, [_P, _P, C.c_int32, C.c_int32, _P, _P]),
     "tomatis_ts_gate": (C.c_int, [_P, _P, _P, C.c_int32, C.c_int32, _P, _P, _P]),
     "tomatis_plan_error": (C.c_int, [_P, _P]),
+    "tomatis_plan_error_bits": (C.c_int, [_P, C.POINTER(C.c_uint32), C.c_int32, _P]),
+    "tomatis_plan_set_option": (C.c_int, [_P, C.c_int32, C.c_int64]),
     "tomatis_absmax": (C.c_int, [_P, C.c_int64, _P, _P]),
     "tomatis_absmax_streams": (C.c_int, [_P, _P, _P, _P]),
     "tomatis_scale_copy": (C.c_int, [_P, _P, C.c_int64, C.c_float, _P]),

@@ -59,45 +59,11 @@ constexpr double ct_sin2pi(long m, long M) { return ct_cos2pi(m - M / 4, M); }  
 // ---------------------------------------------------------------------------
 // complex float in registers
 // ---------------------------------------------------------------------------
-#ifdef TM_VCF
-// experiment: complex values as a packed-fp32 vector pair (v_pk_* arithmetic)
-typedef float cf __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ cf fma2(cf a, cf b, cf c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ cf cmul(cf a, cf w) {  // a * w: v_pk_mul + v_pk_fma
-  cf t, r;
-  __asm__("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0] neg_lo:[0,1]"
-          : "=v"(t) : "v"(a), "v"(w));
-  __asm__("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(r) : "v"(a), "v"(w), "v"(t));
-  return r;
-}
-__device__ __forceinline__ cf cmulc(cf a, cf w) {  // a * conj(w)
-  cf t, r;
-  __asm__("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0]" : "=v"(t) : "v"(a), "v"(w));
-  __asm__("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] neg_hi:[0,1,0]"
-          : "=v"(r) : "v"(a), "v"(w), "v"(t));
-  return r;
-}
-__device__ __forceinline__ cf cscale(cf a, float s) { return a * s; }
-#else
 struct cf {
   float x, y;
 };
-#endif
-#if defined(TM_PACKED) && !defined(TM_VCF)  // complex add/sub as one v_pk_add_f32 (gfx950 packed fp32)
-typedef float f2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ cf operator+(cf a, cf b) {
-  const f2v r = f2v{a.x, a.y} + f2v{b.x, b.y};
-  return {r.x, r.y};
-}
-__device__ __forceinline__ cf operator-(cf a, cf b) {
-  const f2v r = f2v{a.x, a.y} - f2v{b.x, b.y};
-  return {r.x, r.y};
-}
-#elif !defined(TM_VCF)
 __device__ __forceinline__ cf operator+(cf a, cf b) { return {a.x + b.x, a.y + b.y}; }
 __device__ __forceinline__ cf operator-(cf a, cf b) { return {a.x - b.x, a.y - b.y}; }
-#endif
-#ifndef TM_VCF
 __device__ __forceinline__ cf cmul(cf a, cf w) {  // a * w
   return {__builtin_fmaf(a.x, w.x, -(a.y * w.y)), __builtin_fmaf(a.x, w.y, a.y * w.x)};
 }
@@ -105,7 +71,6 @@ __device__ __forceinline__ cf cmulc(cf a, cf w) {  // a * conj(w)
   return {__builtin_fmaf(a.x, w.x, a.y * w.y), __builtin_fmaf(a.y, w.x, -(a.x * w.y))};
 }
 __device__ __forceinline__ cf cscale(cf a, float s) { return {a.x * s, a.y * s}; }
-#endif
 
 // multiply by W_M^m = exp(-+2*pi*i*m/M) (forward: minus, INV: plus), m,M compile-time
 template <int M, int m, bool INV>
@@ -334,22 +299,12 @@ __device__ __forceinline__ void sdft(cf (&v)[NT]) {
         v[OFF + o.b] = A - B;
       } else if constexpr (o.big == 0) {
         constexpr float r = (float)o.r;
-#ifdef TM_VCF
-        v[OFF + o.a] = fma2(B, cf{r, r}, A);
-        v[OFF + o.b] = fma2(B, cf{-r, -r}, A);
-#else
         v[OFF + o.a] = {__builtin_fmaf(B.x, r, A.x), __builtin_fmaf(B.y, r, A.y)};
         v[OFF + o.b] = {__builtin_fmaf(B.x, -r, A.x), __builtin_fmaf(B.y, -r, A.y)};
-#endif
       } else {
         constexpr float r = (float)o.r;
-#ifdef TM_VCF
-        v[OFF + o.a] = fma2(A, cf{r, r}, B);
-        v[OFF + o.b] = fma2(A, cf{r, r}, -B);
-#else
         v[OFF + o.a] = {__builtin_fmaf(A.x, r, B.x), __builtin_fmaf(A.y, r, B.y)};
         v[OFF + o.b] = {__builtin_fmaf(A.x, r, -B.x), __builtin_fmaf(A.y, r, -B.y)};
-#endif
       }
     } else if constexpr (o.kind == 2) {
       const cf x = v[OFF + o.a];
@@ -362,14 +317,6 @@ __device__ __forceinline__ void sdft(cf (&v)[NT]) {
       const cf x = v[OFF + o.a];
       constexpr float t = (float)o.r;
       const float sx = o.sg > 0 ? x.x : -x.x, sy = o.sg > 0 ? x.y : -x.y;
-#ifdef TM_VCF
-      const cf sxy = o.sg > 0 ? x : -x;
-      if constexpr (o.form == 0) {   // |c| [(sc x - t y) + i (sc y + t x)]
-        v[OFF + o.a] = fma2(x.yx, cf{-t, t}, sxy);
-      } else {                       // |s| [(ct x - ss y) + i (ct y + ss x)]
-        v[OFF + o.a] = fma2(x, cf{t, t}, sxy.yx * cf{-1.f, 1.f});
-      }
-#else
       if constexpr (o.form == 0) {   // |c| [(sc x - t y) + i (sc y + t x)]
         if constexpr (t == 1.0f) v[OFF + o.a] = {sx - x.y, sy + x.x};
         else if constexpr (t == -1.0f) v[OFF + o.a] = {sx + x.y, sy - x.x};
@@ -377,7 +324,6 @@ __device__ __forceinline__ void sdft(cf (&v)[NT]) {
       } else {                       // |s| [(ct x - ss y) + i (ct y + ss x)]
         v[OFF + o.a] = {__builtin_fmaf(t, x.x, -sy), __builtin_fmaf(t, x.y, sx)};
       }
-#endif
     }
   });
   cf tt[M];

@@ -16,55 +16,9 @@
 // cover k2 blocks of PB so a round reads back exactly the registers it wrote.
 #pragma once
 #include "tm_common.h"
+#include "../../include/tomatis_hip.h"  // TOMATIS_ERR_* bits
 
 namespace tdsp {
-
-// scheduling fence between FFT steps: keeps each step's LDS table reads next to
-// their use instead of hoisted a whole step ahead (register pressure; the other
-// waves on the SIMD hide the latency)
-// timing experiments only (wrong results): TM_EXP_NOTAB reads every per-lane
-// table at one index (the loads CSE away), TM_EXP_NOXCH skips the exchanges
-#ifdef TM_EXP_NOTAB
-#define TM_TI(i) (L)
-#else
-#define TM_TI(i) (i)
-#endif
-#if defined(TM_EXP_NOTAB) || defined(TM_EXP_NOTAB_TW)
-#define TM_TIW(i) (L)
-#else
-#define TM_TIW(i) (i)
-#endif
-#if defined(TM_EXP_NOTAB) || defined(TM_EXP_NOTAB_P)
-#define TM_TIP(i) (L)
-#else
-#define TM_TIP(i) (i)
-#endif
-#if defined(TM_EXP_NOTAB) || defined(TM_EXP_NOTAB_W) || defined(TM_EXP_NOTAB_WA)
-#define TM_TIN(i) (L)
-#else
-#define TM_TIN(i) (i)
-#endif
-#if defined(TM_EXP_NOTAB) || defined(TM_EXP_NOTAB_W) || defined(TM_EXP_NOTAB_WS)
-#define TM_TINS(i) (L)
-#else
-#define TM_TINS(i) (i)
-#endif
-#if defined(TM_EXP_NOTAB) || defined(TM_EXP_NOTAB_G)
-#define TM_TIG(i) (L)
-#else
-#define TM_TIG(i) (i)
-#endif
-#ifdef TM_EXP_NOXCH
-#define TM_XCH if constexpr (false)
-#else
-#define TM_XCH
-#endif
-
-#if defined(TM_SB)
-#define TM_STEP_FENCE() __builtin_amdgcn_sched_barrier(0)
-#else
-#define TM_STEP_FENCE()
-#endif
 
 template <int P_, int NR_ = 32>
 struct FftGeo {
@@ -81,10 +35,6 @@ struct FftGeo {
   static constexpr int SEQ_LDS = BUF + (P > 64 ? 1 : 0);
   static_assert(PB >= 4 && PB <= NR && NR % 8 == 0, "need 4 <= P/8 <= NR, NR % 8 == 0");
 };
-
-// default for the register step-3b twiddles (unused unless TR)
-__device__ inline constexpr cf kNoTp[8] = {};
-__device__ inline constexpr cf kNoTb[12] = {};
 
 // Barrier of the two waves of a P = 128 sequence (not the whole workgroup):
 // a counter in the sequence's LDS slot.  Both waves add 1 per barrier and can
@@ -105,22 +55,17 @@ __device__ __forceinline__ void pair_barrier(uint32_t* ctr, uint32_t* err) {
     if ((int32_t)(c - target) >= 0) return;
     __builtin_amdgcn_s_sleep(1);
   }
-  if (err && (threadIdx.x & 63) == 0) atomicOr(err, 2u);
+  if (err && (threadIdx.x & 63) == 0) atomicOr(err, TOMATIS_ERR_PAIR_BARRIER);
 }
 
 // LDS synchronisation for an exchange: wave-local when P == 64, the pair
 // barrier when P == 128 (counter at buf[BUF]), else the workgroup barrier.
 template <int P, int NR = 32>
 __device__ __forceinline__ void xsync(cf* buf = nullptr, uint32_t* err = nullptr) {
-#ifdef TM_EXP_NOSYNC  // timing experiments only (wrong results): no exchange ordering
-  if constexpr (P <= 64) return;
-#endif
-#ifndef TM_NO_PAIRSYNC
   if constexpr (P == 128) {
     pair_barrier(reinterpret_cast<uint32_t*>(buf + FftGeo<P, NR>::BUF), err);
     return;
   }
-#endif
   if constexpr (P <= 64) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -139,42 +84,24 @@ __device__ __forceinline__ int x2col(int a, int c) { return 8 * c + (a ^ (c & 7)
 // LT: twP is the per-lane table W_P^{(L%8)*m} for m < 8 in lane-pair layout
 // [m/2][L][m&1] (P == 64 only: one ds_read_b128 per two twiddles, one address
 // VGPR instead of seven)
-template <int P, int NR = 32, bool LT = false, bool TR = false, bool TN = false>
+template <int P, int NR = 32, bool LT = false>
 __device__ __forceinline__ void fft_fwd(cf (&v)[NR], int L, const cf* twN, const cf* twP,
-                                        cf* buf, const cf (&tp)[8] = kNoTp,
-                                        const cf (&tb)[12] = kNoTb, uint32_t* err = nullptr) {
+                                        cf* buf, uint32_t* err = nullptr) {
   using G = FftGeo<P, NR>;
   constexpr int PB = G::PB, RW = G::RW;
   const int a1 = L & 7, q1 = L >> 3;
   const int c3 = L % PB, q3 = L / PB;
-  if constexpr (TN) {
-    // step 1 unscaled; step 2 twiddle W_N^{L k2} = W_N^{8aL} W_N^{bL} (k2 = 8a + b)
-    // from register bases tb[b] = W_N^{bL} (b < 8), tb[8 + a] = W_N^{8aL}
-    dft<NR, false, 0, 1, NR>(v);
-    TM_STEP_FENCE();
-    sfor<1, NR>([&](auto kk) {
-      constexpr int K2 = decltype(kk)::value;
-      constexpr int a = K2 / 8, b = K2 % 8;
-      if constexpr (a == 0) v[K2] = cmul(v[K2], tb[b]);
-      else if constexpr (b == 0) v[K2] = cmul(v[K2], tb[8 + a]);
-      else v[K2] = cmul(cmul(v[K2], tb[8 + a]), tb[b]);
-    });
-  } else {
   // step 1 (outputs carry splan<NR, 0>().sig: the twN table absorbs them)
-#ifndef TM_EXP_SKIP1F  // timing experiments only (wrong results): no step-1 DFT
   sdft<NR, 0, 0, NR>(v);
-#endif
-  TM_STEP_FENCE();
   // step 2 (twiddles in lane-pair layout: one ds_read_b128 per two registers)
   sfor<0, NR / 2>([&](auto kk) {
     constexpr int K2 = decltype(kk)::value;
-    const float4 t = reinterpret_cast<const float4*>(twN)[TM_TIW(K2 * P + L)];
+    const float4 t = reinterpret_cast<const float4*>(twN)[K2 * P + L];
     if constexpr (K2 > 0) v[2 * K2] = cmul(v[2 * K2], cf{t.x, t.y});
     v[2 * K2 + 1] = cmul(v[2 * K2 + 1], cf{t.z, t.w});
   });
-  }
   // exchange 1 : (lane n1, reg k2) -> (lane (a,q), reg (j,b))
-  TM_XCH sfor<0, G::ROUNDS>([&](auto rr) {
+  sfor<0, G::ROUNDS>([&](auto rr) {
     constexpr int R = decltype(rr)::value;
     sfor<0, PB>([&](auto kk) {
       constexpr int K = decltype(kk)::value;
@@ -187,29 +114,18 @@ __device__ __forceinline__ void fft_fwd(cf (&v)[NR], int L, const cf* twN, const
     });
     xsync<P, NR>(buf, err);
   });
-  TM_STEP_FENCE();
   // step 3a: DFT_PB over b for each j (output c carries splan<PB, 0>().sig[c],
   // absorbed by the step-3b twiddles)
   sfor<0, G::NJ>([&](auto jj) {
     constexpr int J = decltype(jj)::value;
     sdft<PB, 0, J * PB, NR>(v);
   });
-  TM_STEP_FENCE();
   // step 3b: W_P^{a c}
-  if constexpr (TR) {  // the same per-lane twiddles, held in registers (tp[c])
-    static_assert(PB == 8, "register twiddles need P == 64");
-    sfor<1, 8>([&](auto cc) {
-      constexpr int C = decltype(cc)::value;
-      sfor<0, G::NJ>([&](auto jj) {
-        constexpr int J = decltype(jj)::value;
-        v[J * PB + C] = cmul(v[J * PB + C], tp[C]);
-      });
-    });
-  } else if constexpr (LT) {
+  if constexpr (LT) {
     static_assert(PB == 8, "lane twiddle table needs P == 64");
     sfor<0, 4>([&](auto cc) {
       constexpr int C2 = decltype(cc)::value;
-      const float4 t = reinterpret_cast<const float4*>(twP)[TM_TIP(C2 * P + L)];
+      const float4 t = reinterpret_cast<const float4*>(twP)[C2 * P + L];
       sfor<0, G::NJ>([&](auto jj) {
         constexpr int J = decltype(jj)::value;
         if constexpr (C2 > 0) v[J * PB + 2 * C2] = cmul(v[J * PB + 2 * C2], cf{t.x, t.y});
@@ -228,7 +144,7 @@ __device__ __forceinline__ void fft_fwd(cf (&v)[NR], int L, const cf* twN, const
     });
   }
   // exchange 2 : (lane (a,q), reg (j,c)) -> (lane (c,q'), reg (j',a))
-  TM_XCH sfor<0, G::ROUNDS>([&](auto rr) {
+  sfor<0, G::ROUNDS>([&](auto rr) {
     constexpr int R = decltype(rr)::value;
     sfor<0, PB>([&](auto cc) {
       constexpr int C = decltype(cc)::value;
@@ -245,7 +161,6 @@ __device__ __forceinline__ void fft_fwd(cf (&v)[NR], int L, const cf* twN, const
     });
     xsync<P, NR>(buf, err);
   });
-  TM_STEP_FENCE();
   // step 3c: DFT_8 over a (output d carries splan<8, 0>().sig[d], absorbed by
   // the per-lane gain rows, k_gain_perm)
   sfor<0, NR / 8>([&](auto jj) {
@@ -255,10 +170,9 @@ __device__ __forceinline__ void fft_fwd(cf (&v)[NR], int L, const cf* twN, const
 }
 
 // inverse (unnormalised) FFT: bin layout -> v[n2] = x[L + P*n2] * N
-template <int P, int NR = 32, bool LT = false, bool TR = false, bool TN = false>
+template <int P, int NR = 32, bool LT = false>
 __device__ __forceinline__ void fft_inv(cf (&v)[NR], int L, const cf* twN, const cf* twP,
-                                        cf* buf, const cf (&tp)[8] = kNoTp,
-                                        const cf (&tb)[12] = kNoTb, uint32_t* err = nullptr) {
+                                        cf* buf, uint32_t* err = nullptr) {
   using G = FftGeo<P, NR>;
   constexpr int PB = G::PB, RW = G::RW;
   const int a1 = L & 7, q1 = L >> 3;
@@ -270,20 +184,11 @@ __device__ __forceinline__ void fft_inv(cf (&v)[NR], int L, const cf* twN, const
     constexpr int J = decltype(jj)::value;
     sdft<8, 1, J * 8, NR>(v);
   });
-  TM_STEP_FENCE();
   // step 3b': conj W_P^{a c3}
-  if constexpr (TR) {
-    sfor<1, 8>([&](auto aa) {
-      constexpr int A = decltype(aa)::value;
-      sfor<0, NR / 8>([&](auto jj) {
-        constexpr int J = decltype(jj)::value;
-        v[J * 8 + A] = cmulc(v[J * 8 + A], tp[A]);
-      });
-    });
-  } else if constexpr (LT) {  // c3 = L % 8 here: same table as the forward step 3b
+  if constexpr (LT) {  // c3 = L % 8 here: same table as the forward step 3b
     sfor<0, 4>([&](auto aa) {
       constexpr int A2 = decltype(aa)::value;
-      const float4 t = reinterpret_cast<const float4*>(twP)[TM_TIP(A2 * P + L)];
+      const float4 t = reinterpret_cast<const float4*>(twP)[A2 * P + L];
       sfor<0, NR / 8>([&](auto jj) {
         constexpr int J = decltype(jj)::value;
         if constexpr (A2 > 0) v[J * 8 + 2 * A2] = cmulc(v[J * 8 + 2 * A2], cf{t.x, t.y});
@@ -302,7 +207,7 @@ __device__ __forceinline__ void fft_inv(cf (&v)[NR], int L, const cf* twN, const
     });
   }
   // exchange 3 : (lane (c,q'), reg (j',a)) -> (lane (a,q), reg (j,c))
-  TM_XCH sfor<0, G::ROUNDS>([&](auto rr) {
+  sfor<0, G::ROUNDS>([&](auto rr) {
     constexpr int R = decltype(rr)::value;
     sfor<0, PB / 8>([&](auto jj) {
       constexpr int JJ = decltype(jj)::value;
@@ -319,14 +224,13 @@ __device__ __forceinline__ void fft_inv(cf (&v)[NR], int L, const cf* twN, const
     });
     xsync<P, NR>(buf, err);
   });
-  TM_STEP_FENCE();
   // step 3a': IDFT_PB over c -> b
   sfor<0, G::NJ>([&](auto jj) {
     constexpr int J = decltype(jj)::value;
     dft<PB, true, J * PB, 1, NR>(v);
   });
   // exchange 4 : (lane (a,q), reg (j,b)) -> (lane n1, reg k2)
-  TM_XCH sfor<0, G::ROUNDS>([&](auto rr) {
+  sfor<0, G::ROUNDS>([&](auto rr) {
     constexpr int R = decltype(rr)::value;
     sfor<0, PB>([&](auto bb) {
       constexpr int B = decltype(bb)::value;
@@ -339,34 +243,18 @@ __device__ __forceinline__ void fft_inv(cf (&v)[NR], int L, const cf* twN, const
     });
     xsync<P, NR>(buf, err);
   });
-  TM_STEP_FENCE();
-  if constexpr (TN) {
-    sfor<1, NR>([&](auto kk) {
-      constexpr int K2 = decltype(kk)::value;
-      constexpr int a = K2 / 8, b = K2 % 8;
-      if constexpr (a == 0) v[K2] = cmulc(v[K2], tb[b]);
-      else if constexpr (b == 0) v[K2] = cmulc(v[K2], tb[8 + a]);
-      else v[K2] = cmulc(cmulc(v[K2], tb[8 + a]), tb[b]);
-    });
-    TM_STEP_FENCE();
-    dft<NR, true, 0, 1, NR>(v);  // unscaled step 1'
-    return;
-  }
   // step 2': conj W_N^{n1 k2}
   sfor<0, NR / 2>([&](auto kk) {
     constexpr int K2 = decltype(kk)::value;
-    const float4 t = reinterpret_cast<const float4*>(twN)[TM_TIW(K2 * P + L)];
+    const float4 t = reinterpret_cast<const float4*>(twN)[K2 * P + L];
     if constexpr (K2 > 0) v[2 * K2] = cmulc(v[2 * K2], cf{t.x, t.y});
     v[2 * K2 + 1] = cmulc(v[2 * K2 + 1], cf{t.z, t.w});
   });
-  TM_STEP_FENCE();
   // step 1': IDFT_NR over k2 -> n2.  The scaled twN table multiplied register
   // k2 by splan<NR, 0>().sig[k2] on top of the twiddle, so the inputs carry
   // 1 / that (plan 2); the outputs carry splan<NR, 2>().sig[n2], absorbed by
   // the synthesis window (winS).
-#ifndef TM_EXP_SKIP1I
   sdft<NR, 2, 0, NR>(v);
-#endif
 }
 
 // per-lane register tables (window, gains, 1/wsum) in lane-quad layout:

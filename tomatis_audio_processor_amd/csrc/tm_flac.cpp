@@ -667,6 +667,21 @@ void decode_range(const uint8_t* d, size_t len, size_t lo, size_t hi, bool exact
   }
 }
 
+// The threads' frame ranges must tile the decoded samples: every non-empty
+// thread's first frame starts where the previous non-empty thread's last frame
+// ended.  A thread's sync search skips a frame that starts with a sync code but
+// fails its CRC; without this check that frame's samples would be a silent gap
+// (left as whatever the output buffer held).
+int check_contiguous(int nt, const std::vector<int64_t>& begs, const std::vector<int64_t>& ends) {
+  int64_t prev_end = -1;
+  for (int t = 0; t < nt; ++t) {
+    if (ends[t] <= 0) continue;  // no frame starts in this thread's range
+    if (prev_end >= 0 && begs[t] != prev_end) return TOMATIS_FLAC_E_CRC;
+    prev_end = ends[t];
+  }
+  return TOMATIS_FLAC_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -926,8 +941,10 @@ int tomatis_flac_decode_bytes(const uint8_t* d, int64_t len, int64_t lo, int64_t
   }
   for (auto& x : th) x.join();
   int64_t b = INT64_MAX, e = 0;
-  for (int t = 0; t < nt; ++t) {
+  for (int t = 0; t < nt; ++t)
     if (rcs[t]) return rcs[t];
+  if ((rc = check_contiguous(nt, begs, ends))) return rc;
+  for (int t = 0; t < nt; ++t) {
     if (ends[t] > 0) {
       e = std::max(e, ends[t]);
       b = std::min(b, begs[t]);
@@ -964,23 +981,23 @@ int tomatis_flac_decode(const uint8_t* d, int64_t len, int32_t* pcm, int64_t max
   if (const char* e = getenv("TOMATIS_FLAC_THREADS")) nt = std::max(1, atoi(e));
   nt = (int)std::max<size_t>(1, std::min<size_t>(nt, body / (1u << 20)));
   std::vector<int> rcs(nt);
-  std::vector<int64_t> ends(nt);
+  std::vector<int64_t> ends(nt), begs(nt);
   std::vector<std::thread> th;
   for (int t = 0; t < nt; ++t) {
     const size_t lo = p + body * t / nt, hi = p + body * (t + 1) / nt;
     if (t == nt - 1)
       decode_range(d, (size_t)len, lo, (size_t)len, t == 0, ch0, bps0, nominal, total, pcm,
-                   max_frames, &rcs[t], &ends[t]);
+                   max_frames, &rcs[t], &ends[t], &begs[t]);
     else
       th.emplace_back(decode_range, d, (size_t)len, lo, hi, t == 0, ch0, bps0, nominal, total,
-                      pcm, max_frames, &rcs[t], &ends[t], (int64_t*)nullptr);
+                      pcm, max_frames, &rcs[t], &ends[t], &begs[t]);
   }
   for (auto& x : th) x.join();
   int64_t done = 0;
-  for (int t = 0; t < nt; ++t) {
+  for (int t = 0; t < nt; ++t)
     if (rcs[t]) return rcs[t];
-    done = std::max(done, ends[t]);
-  }
+  if ((rc = check_contiguous(nt, begs, ends))) return rc;
+  for (int t = 0; t < nt; ++t) done = std::max(done, ends[t]);
   if (total) done = std::min(done, total);
   // counting mode (pcm == NULL, max_frames == 0): the decoded length
   if (frames_out) *frames_out = pcm ? std::min(done, max_frames) : done;

@@ -1255,6 +1255,8 @@ struct tomatis_plan_s {
   int fuse_span = 0;  // max runs contributing to one chunk
   int64_t run_slots = 0;  // resident sequences of the fused kernel
   int edge_mask = 0;      // set for one tomatis_stft_ola_limited_edges call
+  int fuse_enabled = 1;   // TOMATIS_OPT_FUSE_LIMITER
+  int lim_spin = 1 << 18; // TOMATIS_OPT_LIMITER_SPIN: fused-limiter wait bound (polls)
   // run-scan gate (exclusive on/off predicates)
   bool gate_excl = false;
   void* gsum = nullptr;
@@ -2080,6 +2082,7 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
   A.chunk_need = p->chunk_need;
   A.chunk_rng = p->chunk_rng;
   A.err = p->err;
+  A.lim_spin = p->lim_spin;
   A.prof = nullptr;
   if (limit > 0.f) {
     if (!p->chunk_done) return TOMATIS_E_UNSUPPORTED;
@@ -2149,7 +2152,7 @@ int tomatis_stft_ola_limited_edges(tomatis_plan_t p, const float* x, const float
                                    int32_t n_rows, const uint16_t* rows, float* y,
                                    uint32_t* peaks, float limit, int32_t edge_mask, void* hs) {
   if (!p || !(limit > 0.f) || edge_mask < 0 || edge_mask > 3) return TOMATIS_E_ARG;
-  const bool fuse = !p->generic && p->chunk_done && p->fuse_span > 0 &&
+  const bool fuse = !p->generic && p->chunk_done && p->fuse_span > 0 && p->fuse_enabled &&
                     p->fuse_span <= fuse_max_span(p) && env_int("TOMATIS_FUSE_LIMITER", 1) != 0;
   p->edge_mask = edge_mask;
   int rc;
@@ -2170,11 +2173,35 @@ int tomatis_stft_ola_limited(tomatis_plan_t p, const float* x, const float* gain
 }
 
 int tomatis_plan_error(tomatis_plan_t p, void* hs) {
-  if (!p || !p->err) return TOMATIS_E_ARG;
+  uint32_t e = 0;
+  const int rc = tomatis_plan_error_bits(p, &e, 0, hs);
+  if (rc) return rc;
+  return e ? TOMATIS_E_HIP : TOMATIS_OK;
+}
+
+int tomatis_plan_error_bits(tomatis_plan_t p, uint32_t* bits, int32_t reset, void* hs) {
+  if (!p || !p->err || !bits) return TOMATIS_E_ARG;
   uint32_t e = 0;
   if (hipMemcpyAsync(&e, p->err, 4, hipMemcpyDeviceToHost, (hipStream_t)hs)) return TOMATIS_E_HIP;
   if (hipStreamSynchronize((hipStream_t)hs)) return TOMATIS_E_HIP;
-  return e ? TOMATIS_E_HIP : TOMATIS_OK;
+  *bits = e;
+  if (reset && e) {
+    if (hipMemsetAsync(p->err, 0, 4, (hipStream_t)hs)) return TOMATIS_E_HIP;
+    if (hipStreamSynchronize((hipStream_t)hs)) return TOMATIS_E_HIP;
+  }
+  return TOMATIS_OK;
+}
+
+int tomatis_plan_set_option(tomatis_plan_t p, int32_t option, int64_t value) {
+  if (!p) return TOMATIS_E_ARG;
+  switch (option) {
+    case TOMATIS_OPT_FUSE_LIMITER: p->fuse_enabled = value != 0; return TOMATIS_OK;
+    case TOMATIS_OPT_LIMITER_SPIN:
+      if (value < 0 || value > (1 << 24)) return TOMATIS_E_ARG;
+      p->lim_spin = (int)value;
+      return TOMATIS_OK;
+    default: return TOMATIS_E_ARG;
+  }
 }
 
 int tomatis_apply_limiter(tomatis_plan_t p, float* y, const uint32_t* peaks, float limit, void* hs) {

@@ -54,7 +54,8 @@ struct MainArgs {
   uint32_t* chunk_done;
   const uint32_t* chunk_need;
   const int64_t* chunk_rng;  // [2 * chunk]: output-relative [p0, p1)
-  uint32_t* err;
+  uint32_t* err;        // TOMATIS_ERR_* bits
+  int lim_spin;         // fused-limiter wait bound (polls of the chunk counter)
   unsigned long long* prof;  // TM_PROFILE builds only: per-phase wave cycles
 };
 

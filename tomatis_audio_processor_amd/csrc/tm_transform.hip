@@ -4,17 +4,12 @@
 // max-memory-clause and the iterative strategies measured within 1 %).
 // Reference: src/process_tomatis.py:394-406,419-426,451-453 (see tm_kernels.hip).
 //
-// Build switches (none set in the product build; DESIGN.md §6 has the numbers):
-//   development  TM_DEV_ONE_KERNEL, TM_DEV_ONLY_2048_512, TM_DEV_WG (one
-//                instantiation, 15 s builds), TM_PROFILE (per-phase cycles)
-//   alternatives TM_FLUSH_TOP, TM_NH_DIRECT (3 waves/SIMD spill-free with
-//                TM_DEV_WG=768), TM_TPREG / TM_WREG / TM_TNREG (register-
-//                resident tables), TM_VCF (packed fp32 complex, tm_common.h),
-//                TM_NO_PAIRSYNC (workgroup barriers for two-wave frames),
-//                TM_ST_CACHED / TM_LIM_CACHED (cache policy of the output and
-//                of the limiter's re-reads)
-//   timing only  TM_EXP_* (results are wrong on purpose: missing loads, stores,
-//                exchanges, tables or DFTs, or s_nop padding)
+// Build switches (none set in the product build): TM_DEV_ONE_KERNEL,
+// TM_DEV_ONLY_2048_512, TM_DEV_WG (one instantiation, 15 s development builds)
+// and TM_PROFILE (per-phase cycles of the interior loop).  The alternatives
+// measured and rejected in rounds 1-2 (register-resident tables, packed fp32,
+// cache policies, flush placement, timing-only variants) are in git history
+// and their numbers in DESIGN.md §6.
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -93,14 +88,15 @@ __device__ void limit_own(const MainArgs& A, const TomatisStream& S, int gc, int
                           int64_t hi, int lane) {
   const uint32_t need = A.chunk_need[gc];
   uint32_t got = 0;
-  for (int spin = 0; spin < (1 << 18); ++spin) {
+  for (int spin = 0; spin < A.lim_spin; ++spin) {
     got = __hip_atomic_load(A.chunk_done + gc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     got = __builtin_amdgcn_readfirstlane(got);
     if (got >= need) break;
     __builtin_amdgcn_s_sleep(32);
   }
-  if (got < need) {  // never expected; leaves the chunk unscaled and reports it
-    if (lane == 0) atomicOr(A.err, 1u);
+  if (got < need) {  // never expected; leaves the chunk unscaled and reports it (the
+    // host re-runs the launch unfused, engine.py _finish)
+    if (lane == 0) atomicOr(A.err, TOMATIS_ERR_LIMITER_WAIT);
     return;
   }
   const float peak = __uint_as_float(__builtin_amdgcn_readfirstlane(
@@ -124,11 +120,7 @@ __device__ void limit_own(const MainArgs& A, const TomatisStream& S, int gc, int
     f4v t[U];
 #pragma unroll
     for (int u = 0; u < U; ++u)
-#ifdef TM_LIM_CACHED  // experiment: limiter re-reads through the caches
-      if (i + 64 * u < n4) t[u] = b4[i + 64 * u];
-#else
       if (i + 64 * u < n4) t[u] = __builtin_nontemporal_load(b4 + i + 64 * u);
-#endif
 #pragma unroll
     for (int u = 0; u < U; ++u)
       if (i + 64 * u < n4) __builtin_nontemporal_store(t[u] * sc, b4 + i + 64 * u);
@@ -249,45 +241,6 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   __syncthreads();
   const float4* const w4 = reinterpret_cast<const float4*>(s_win);
   const float4* const ws4 = reinterpret_cast<const float4*>(s_winS);
-  // register-resident per-lane tables (TM_WREG: analysis window, the synthesis
-  // window derived with the inverse's compile-time output scales; TM_TPREG:
-  // step-3b twiddles): LDS reads are the kernel's bottleneck, VGPRs are not
-  constexpr bool kTR = LT
-#ifdef TM_TPREG
-      ;
-#else
-      && false;
-#endif
-  cf tp[8];
-  tp[0] = cf{1.f, 0.f};
-  if constexpr (kTR) {
-#pragma unroll
-    for (int m = 1; m < 8; ++m)
-      tp[m] = cscale(A.twP[((threadIdx.x % P & 7) * m) & (P - 1)], sig_at<8>(m));
-  }
-#ifdef TM_TNREG
-  static_assert(P == 64 && NR == 32, "register step-2 bases: n_fft 2048");
-  constexpr bool kTN = LT;
-  cf tb[12];
-  {
-    const int l = threadIdx.x % P;
-#pragma unroll
-    for (int j = 0; j < 12; ++j) {
-      const int e = j < 8 ? l * j : l * 8 * (j - 8);  // exponent of W_N
-      double sn, cs;
-      sincos(-2.0 * 3.14159265358979323846 * (double)(e % N) / (double)N, &sn, &cs);
-      tb[j] = cf{(float)cs, (float)sn};
-    }
-  }
-#else
-  constexpr bool kTN = false;
-  cf tb[12];
-#endif
-#ifdef TM_WREG
-  float wr[NR];
-#pragma unroll
-  for (int i = 0; i < NR; ++i) wr[i] = A.win[threadIdx.x % P + P * i];
-#endif
 #ifdef TM_PROFILE
   const unsigned long long t_k1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -303,17 +256,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   }
   const TomatisStream S = A.st[R.s];
   const int64_t kfirst = max<int64_t>(0, R.ka - (A.rmax - 1));
-  int nit = valid ? (int)(R.kb - kfirst) : 0;
-#ifdef TM_NO_PAIRSYNC
-  if constexpr (P > 64) {  // the block's sequences share barriers: same trip count
-    __shared__ int s_nit[NSEQ];
-    if (L == 0) s_nit[seq] = nit;
-    __syncthreads();
-    int m = 0;
-    for (int i = 0; i < NSEQ; ++i) m = max(m, s_nit[i]);
-    nit = m;
-  }
-#endif
+  const int nit = valid ? (int)(R.kb - kfirst) : 0;
   cf* buf = s_buf[seq];
   const float* xs = A.x + S.in_off;
   float* ys = A.y + S.out_off;
@@ -352,21 +295,16 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   #pragma unroll
         for (int n2 = 0; n2 < NR; ++n2) v[n2] = cscale(v[n2], iscale);
       }
-#ifdef TM_WREG
-  #pragma unroll
-      for (int i = 0; i < NR; ++i) v[i] = cscale(v[i], wr[i]);
-#else
   #pragma unroll
       for (int n4 = 0; n4 < NR / 4; ++n4) {
-        const float4 w = w4[TM_TIN(n4 * P + L)];
+        const float4 w = w4[n4 * P + L];
         v[4 * n4] = cscale(v[4 * n4], w.x);
         v[4 * n4 + 1] = cscale(v[4 * n4 + 1], w.y);
         v[4 * n4 + 2] = cscale(v[4 * n4 + 2], w.z);
         v[4 * n4 + 3] = cscale(v[4 * n4 + 3], w.w);
       }
-#endif
       TPROF(1, v[NR - 1].x);
-      fft_fwd<P, NR, LT, kTR, kTN>(v, L, s_twN, s_twP, buf, tp, tb, A.err);
+      fft_fwd<P, NR, LT>(v, L, s_twN, s_twP, buf, A.err);
       TPROF(2, v[NR - 1].x);
       // ---- gain row (real, even, 1/N folded in), per-lane layout ----
       bool g_lds = GM == 1;
@@ -376,7 +314,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
             reinterpret_cast<const float4*>(s_gain + ((GM == 1 ? row : row == A.lds_row[1]) ? N : 0));
   #pragma unroll
         for (int n4 = 0; n4 < NR / 4; ++n4) {
-          const float4 g = g4[TM_TIG(n4 * P + L)];
+          const float4 g = g4[n4 * P + L];
           v[4 * n4] = cscale(v[4 * n4], g.x);
           v[4 * n4 + 1] = cscale(v[4 * n4 + 1], g.y);
           v[4 * n4 + 2] = cscale(v[4 * n4 + 2], g.z);
@@ -394,22 +332,13 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
         }
       }
       TPROF(3, v[NR - 1].x);
-      fft_inv<P, NR, LT, kTR, kTN>(v, L, s_twN, s_twP, buf, tp, tb, A.err);
+      fft_inv<P, NR, LT>(v, L, s_twN, s_twP, buf, A.err);
       TPROF(4, v[NR - 1].x);
       // ---- synthesis window (x the inverse FFT's output scales) + register OLA ----
   #pragma unroll
       for (int n4 = 0; n4 < NR / 4; ++n4) {
-#ifdef TM_WREG
-        // unscaled step 1' (TM_TNREG): the plain window
-        constexpr bool kU = kTN;
-        const float ww[4] = {kU ? wr[4 * n4] : wr[4 * n4] * (float)splan<NR, 2>().sig[4 * n4],
-                             kU ? wr[4 * n4 + 1] : wr[4 * n4 + 1] * (float)splan<NR, 2>().sig[4 * n4 + 1],
-                             kU ? wr[4 * n4 + 2] : wr[4 * n4 + 2] * (float)splan<NR, 2>().sig[4 * n4 + 2],
-                             kU ? wr[4 * n4 + 3] : wr[4 * n4 + 3] * (float)splan<NR, 2>().sig[4 * n4 + 3]};
-#else
-        const float4 w = ws4[TM_TINS(n4 * P + L)];
+        const float4 w = ws4[n4 * P + L];
         const float ww[4] = {w.x, w.y, w.z, w.w};
-#endif
   #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int i = 4 * n4 + u;
@@ -426,7 +355,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
     float wv[SHQ];
 #pragma unroll
     for (int q = 0; q < SHQ / 4; ++q) {
-      const float4 t = reinterpret_cast<const float4*>(s_winv)[TM_TIG(q * P + L)];
+      const float4 t = reinterpret_cast<const float4*>(s_winv)[q * P + L];
       wv[4 * q] = t.x;
       wv[4 * q + 1] = t.y;
       wv[4 * q + 2] = t.z;
@@ -490,11 +419,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
     auto store_out = [&](const cf (&o)[SH], __amdgpu_buffer_rsrc_t r, int so) {
 #pragma unroll
       for (int i = 0; i < SH; ++i) {
-#ifdef TM_ST_CACHED  // experiment: output stores through the caches (limiter re-reads)
-        if constexpr (false) bstore<CH, 2>(o[i], r, L * CH * 4, so + P * i * CH * 4);
-#else
         if constexpr (NT) bstore<CH, 2>(o[i], r, L * CH * 4, so + P * i * CH * 4);
-#endif
         else bstore<CH>(o[i], r, L * CH * 4, so + P * i * CH * 4);
       }
     };
@@ -509,39 +434,26 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
 #pragma unroll
       for (int i = 0; i < SH; ++i) o[i] = cf{0.f, 0.f};
       store_out(o, rnull, 0);
-#ifndef TM_NH_DIRECT
       ld_new(min(1, nit - 1), nh);
-#endif
     }
     for (int it = 0; it < nit; ++it) {
       const uint32_t row = row_of(rw_nx, it);
       rw_nx = row_word(min(it + 1, nit - 1));
       const bool emit = it >= nwarm;
-      // a frame that starts a new chunk flushes the previous chunk's peak first
-      // (pk holds frames < k only).  TM_FLUSH_TOP: before the transform, where
-      // few registers are live (after it, the sunk tail of the inverse FFT stays
-      // live across both paths of the branch: peak pressure 252 -> 179 VGPRs)
-#ifdef TM_FLUSH_TOP
-      if (emit && kfirst + it == next_chunk_k) {
-        flush_peak<P>(pk, cid, S, A.peaks, L, done);
-        ++cid;
-        next_chunk_k = (cid < S.n_chunks - 1) ? next_chunk_k + chunk_k_step : INT64_MAX;
-      }
-#endif
       TPROF(0, v[0].x);
       transform(v, row);
       TPROF(5, v[NR - 1].x);
-#ifndef TM_FLUSH_TOP
+      // a frame that starts a new chunk flushes the previous chunk's peak first
+      // (pk holds frames < k only)
       if (emit && kfirst + it == next_chunk_k) {
         flush_peak<P>(pk, cid, S, A.peaks, L, done);
         ++cid;
         next_chunk_k = (cid < S.n_chunks - 1) ? next_chunk_k + chunk_k_step : INT64_MAX;
       }
-#endif
       // outputs of this frame's first hop: interior 1/sum w^2, output scale, peak
 #pragma unroll
       for (int q = 0; q < SHQ / 4; ++q) {
-        const float4 t4 = reinterpret_cast<const float4*>(s_winv)[TM_TIG(q * P + L)];
+        const float4 t4 = reinterpret_cast<const float4*>(s_winv)[q * P + L];
         wv[4 * q] = t4.x;
         wv[4 * q + 1] = t4.y;
         wv[4 * q + 2] = t4.z;
@@ -558,44 +470,15 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       for (int i = 0; i < NC; ++i) acc[i] = v[i + SH];
       // next frame's input (clamped), then this frame's stores, then the new hop
       // of the frame after next
-#if defined(TM_EXP_NO_OLD)  // timing experiments: no reload of the overlap (wrong results)
-#elif defined(TM_EXP_L1LOAD)  // timing experiments: inputs from one L1-resident frame
-      ld_old(0, v);
-#else
       ld_old(min(it + 1, nit - 1), v);
-#endif
-#if defined(TM_NH_DIRECT)  // the next frame's new hop straight from HBM (no prefetch registers)
-      {
-        cf t[SH];
-        ld_new(min(it + 1, nit - 1), t);
-#pragma unroll
-        for (int j = 0; j < SH; ++j) v[NO + j] = t[j];
-      }
-#else
       // the arrived new hop moves into the frame here, through opaque copies: a
       // plain assignment lets the loop-carried copy land after the next
       // prefetch's issue, where it waits for that HBM load
 #pragma unroll
       for (int j = 0; j < SH; ++j) v[NO + j] = cf{opaque_f(nh[j].x), opaque_f(nh[j].y)};
-#endif
-#if defined(TM_EXP_NO_ST)  // timing experiments: no output stores (wrong results)
-      if (it == 0x7fffffff) store_out(o, rnull, 0);
-#elif defined(TM_EXP_NOSTORE)  // timing experiments: outputs dropped
-      store_out(o, rnull, 0);
-#else
       store_out(o, emit ? ry : rnull, emit ? (it - nwarm) * (HOP * CH * 4) : 0);
-#endif
-#if defined(TM_EXP_NO_NEW) || defined(TM_NH_DIRECT)  // (TM_EXP_NO_NEW: wrong results)
-#elif defined(TM_EXP_L1LOAD)
-      ld_new(0, nh);
-#else
       ld_new(min(it + 2, nit - 1), nh);
-#endif
       TPROF(6, acc[0].x);
-#ifdef TM_EXP_NOPS  // diagnostic: N extra 4-byte s_nop per frame (instruction-fetch sensitivity)
-#pragma unroll
-      for (int q = 0; q < TM_EXP_NOPS; ++q) __asm__ volatile("s_nop 0");
-#endif
     }
 #ifdef TM_PROFILE
     if (L == 0) {
@@ -604,7 +487,6 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
     }
 #endif
   } else {
-#ifndef TM_DEV_NO_GENERIC  // timing experiments only: interior loop alone
     // frame loads are software-pipelined one frame ahead (the next frame's HBM/L2
     // latency hides behind this frame's transforms)
     auto load_frame = [&](int64_t kk, cf (&dst)[NR]) {
@@ -695,7 +577,6 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   #pragma unroll
       for (int i = 0; i < NC; ++i) acc[i] = v[i + SH];
     }
-#endif
   }
   if (valid) flush_peak<P>(pk, cid, S, A.peaks, L, done);
   if (valid && done) {
@@ -756,17 +637,7 @@ __global__ __launch_bounds__(256, 2) void k_stft_frames(MainArgs A) {
     if (!valid) return;
   }
   const TomatisStream S = A.st[R.s];
-  int nit = valid ? (int)(R.kb - R.ka) : 0;
-#ifdef TM_NO_PAIRSYNC
-  if constexpr (P > 64) {
-    __shared__ int s_nit[NSEQ];
-    if (L == 0) s_nit[seq] = nit;
-    __syncthreads();
-    int m = 0;
-    for (int i = 0; i < NSEQ; ++i) m = max(m, s_nit[i]);
-    nit = m;
-  }
-#endif
+  const int nit = valid ? (int)(R.kb - R.ka) : 0;
   cf* buf = s_buf[seq];
   const float* xs = A.x + S.in_off;
   const int hop = A.hop;
@@ -786,12 +657,12 @@ __global__ __launch_bounds__(256, 2) void k_stft_frames(MainArgs A) {
       const float w = s_win[L + P * n2];
       v[n2] = {(z.x * S.in_scale) * w, (z.y * S.in_scale) * w};
     }
-    fft_fwd<P, NR>(v, L, s_twN, s_twP, buf, kNoTp, kNoTb, A.err);
+    fft_fwd<P, NR>(v, L, s_twN, s_twP, buf, A.err);
     const uint16_t row = live ? A.rows[S.frame_base + k] : 0;
     const float* g = A.gains + (int64_t)row * N;
 #pragma unroll
     for (int i = 0; i < NR; ++i) v[i] = cscale(v[i], g[lq<P>(i, L)]);
-    fft_inv<P, NR>(v, L, s_twN, s_twP, buf, kNoTp, kNoTb, A.err);
+    fft_inv<P, NR>(v, L, s_twN, s_twP, buf, A.err);
     if (live) {
       cf* dst = A.scratch + (S.frame_base + k) * (int64_t)N;
 #pragma unroll

@@ -18,13 +18,15 @@ from __future__ import annotations
 
 import ctypes as C
 import time
+import warnings
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
 import numpy as np
 
 from . import dsp
-from ._lib import (F32, F64, NORM_EPS, NORM_MAX, TomatisPlanDesc, TomatisStream, check, lib,
+from ._lib import (ERR_LIMITER_WAIT, ERR_PAIR_BARRIER, F32, F64, NORM_EPS, NORM_MAX,
+                   OPT_FUSE_LIMITER, OPT_LIMITER_SPIN, TomatisPlanDesc, TomatisStream, check, lib,
                    ptr, stream_handle)
 
 PEAK_LIMIT = 0.999
@@ -119,6 +121,21 @@ class Plan:
         """Raise if a device-side consistency check fired (synchronises)."""
         check(self.L.tomatis_plan_error(self.h, stream_handle()), "plan_error")
 
+    def error_bits(self, reset: bool = True) -> int:
+        """The plan's device error word (TOMATIS_ERR_* bits; synchronises the
+        current stream), cleared when ``reset``."""
+        b = C.c_uint32(0)
+        check(self.L.tomatis_plan_error_bits(self.h, C.byref(b), 1 if reset else 0,
+                                             stream_handle()), "plan_error_bits")
+        return int(b.value)
+
+    def set_option(self, option: int, value: int):
+        check(self.L.tomatis_plan_set_option(self.h, option, int(value)), "plan_set_option")
+
+    def set_limiter_spin(self, polls: int):
+        """Fused-limiter wait bound (fault injection: 0 forces the recovery path)."""
+        self.set_option(OPT_LIMITER_SPIN, polls)
+
     def close(self):
         if getattr(self, "h", None):
             self.L.tomatis_plan_destroy(self.h)
@@ -129,6 +146,44 @@ class Plan:
             self.close()
         except Exception:
             pass
+
+
+class DeviceCheckError(RuntimeError):
+    """A device-side consistency check fired and the output cannot be trusted."""
+
+
+def finish_plan(plan: Plan, redo, what: str) -> int:
+    """Read (and clear) ``plan``'s device error word after a pass; every product
+    path calls this before it returns (synchronises the current stream).
+
+    * TOMATIS_ERR_LIMITER_WAIT: a fused-limiter wave gave up waiting for its
+      chunk and left its samples unscaled.  ``redo()`` re-launches the pass's
+      transform with the limiter as a separate launch (the kernel's outputs and
+      peaks are deterministic, so the result equals an undisturbed fused run);
+      a warning says so.
+    * TOMATIS_ERR_PAIR_BARRIER (or any bit after the redo): raise.
+    Returns the bits first seen (0 normally)."""
+    bits = plan.error_bits(reset=True)
+    if bits & ERR_PAIR_BARRIER:
+        raise DeviceCheckError(f"{what}: two-wave FFT exchange barrier timed out "
+                               f"(device error bits {bits:#x}); the output is invalid")
+    if bits & ERR_LIMITER_WAIT:
+        if redo is None:
+            raise DeviceCheckError(f"{what}: fused limiter wait timed out (bits {bits:#x})")
+        warnings.warn(f"{what}: fused limiter wait timed out on the device; "
+                      "re-running the transform with the separate limiter launch",
+                      RuntimeWarning, stacklevel=3)
+        plan.set_option(OPT_FUSE_LIMITER, 0)
+        try:
+            redo()
+        finally:
+            plan.set_option(OPT_FUSE_LIMITER, 1)
+        again = plan.error_bits(reset=True)
+        if again:
+            raise DeviceCheckError(f"{what}: device error bits {again:#x} after the unfused re-run")
+    elif bits:
+        raise DeviceCheckError(f"{what}: unknown device error bits {bits:#x}")
+    return bits
 
 
 _POOL = None
@@ -363,25 +418,37 @@ class GatePipeline:
         self.out_offs = out_offs
         self.g1_db, self.g2_db = g1_db, g2_db
 
-    def run(self, marks=None):
-        """Launch the whole chain on the current stream (no host sync).
+    def run(self, marks=None, check_device: bool = True):
+        """Launch the whole chain on the current stream.
 
         ``marks``: optional pair of torch.cuda.Event recorded on this stream
-        around the fused STFT-OLA launch (bench.py's live kernel timing)."""
+        around the fused STFT-OLA launch (bench.py's live kernel timing).
+        ``check_device``: read the plan's device error word before returning
+        (one host synchronisation; ``finish_plan``).  Only a caller that checks
+        once after many passes (bench.py's timed loop) turns it off."""
         L, P, hs = lib(), self.plan.h, stream_handle()
-        self.peaks.zero_()
         check(L.tomatis_levels(P, ptr(self.ss.x), ptr(self.r), F32, hs), "levels")
         check(L.tomatis_gate_std(P, ptr(self.r), ptr(self.states), ptr(self.rows),
                                  ptr(self.alpha), hs), "gate_std")
         if marks:
             marks[0].record()
-        # transform + OLA + per-chunk limiter (fused in-kernel when chunks are short)
-        check(L.tomatis_stft_ola_limited(P, ptr(self.ss.x), ptr(self.gains), self.n_rows,
-                                         ptr(self.rows), ptr(self.y), ptr(self.peaks),
-                                         PEAK_LIMIT, hs), "stft_ola_limited")
+        self._transform()
         if marks:
             marks[1].record()
+        if check_device:
+            self.finish()
         return self.result()
+
+    def _transform(self):
+        """transform + OLA + per-chunk limiter (fused in-kernel when chunks are short)"""
+        self.peaks.zero_()
+        check(lib().tomatis_stft_ola_limited(self.plan.h, ptr(self.ss.x), ptr(self.gains),
+                                             self.n_rows, ptr(self.rows), ptr(self.y),
+                                             ptr(self.peaks), PEAK_LIMIT, stream_handle()),
+              "stft_ola_limited")
+
+    def finish(self) -> int:
+        return finish_plan(self.plan, self._transform, "GatePipeline")
 
     def result(self) -> Result:
         st = self.streams
@@ -481,11 +548,29 @@ class AdaptivePipeline:
         self.n_rows = len(rows)
         self.out_offs = out_offs
 
-    def run(self, marks=None, timer=None):
-        """``timer`` (a dict) collects synchronised wall-clock phases (profiling)."""
+    def run(self, marks=None, timer=None, check_device: bool = True):
+        """``timer`` (a dict) collects synchronised wall-clock phases (profiling).
+        ``check_device``: as GatePipeline.run."""
         for _ in self.steps(marks, timer):
             pass
+        if check_device:
+            self.finish()
         return self.result()
+
+    def _transform(self):
+        """STFT-gain-OLA, normalise max(w,1e-8), restore, global limiter (one
+        chunk per stream: fused into the transform when its runs allow)"""
+        self.peaks.zero_()
+        check(lib().tomatis_stft_ola_limited(self.plan.h, ptr(self.ss.x), ptr(self.gains),
+                                             self.n_rows, ptr(self.rows), ptr(self.y),
+                                             ptr(self.peaks), PEAK_LIMIT, stream_handle()),
+              "stft_ola_limited")
+
+    def finish(self) -> int:
+        """Device error check after the pass (on the pipeline's stream)."""
+        torch = _torch()
+        with torch.cuda.stream(self.stream or torch.cuda.current_stream()):
+            return finish_plan(self.plan, self._transform, "AdaptivePipeline")
 
     def steps(self, marks=None, timer=None, after=None):
         """The pass as a generator that yields wherever the host would wait for
@@ -583,16 +668,12 @@ class AdaptivePipeline:
         yield   # (a driver launches every group's statistics before the transforms)
         with torch.cuda.stream(strm):
             hs = stream_handle()
-            # 4. STFT-gain-OLA, normalise max(w,1e-8), restore, global limiter (one
-            #    chunk per stream: fused into the transform when its runs allow)
-            self.peaks.zero_()
+            # 4. STFT-gain-OLA, normalise, restore, global limiter
             if after is not None and after() is not None:
                 strm.wait_event(after())
             if marks and marks[0] is not None:
                 marks[0].record()
-            check(L.tomatis_stft_ola_limited(P, ptr(ss.x), ptr(self.gains), self.n_rows,
-                                             ptr(self.rows), ptr(self.y), ptr(self.peaks),
-                                             PEAK_LIMIT, hs), "stft_ola_limited")
+            self._transform()
             if marks and marks[1] is not None:
                 marks[1].record()
             self.done.record()
@@ -680,7 +761,7 @@ class AdaptiveGroups:
             self.pipes.append(p)
         self.ss = ss
 
-    def run(self, marks=None):
+    def run(self, marks=None, check_device: bool = True):
         torch = _torch()
         cur = torch.cuda.current_stream()
         for p in self.pipes:
@@ -702,7 +783,15 @@ class AdaptiveGroups:
                     live.remove(gen)
         for p in self.pipes:
             cur.wait_stream(p.stream)
+        if check_device:
+            self.finish()
         return self.result()
+
+    def finish(self) -> int:
+        bits = 0
+        for p in self.pipes:
+            bits |= p.finish()
+        return bits
 
     def result(self) -> Result:
         return merge_results([p.result() for p in self.pipes])
@@ -748,7 +837,7 @@ class StaticEqPipeline:
         self.gains = torch.from_numpy(np.asarray(gain_bins, np.float32)[None, :].copy()).to(dev)
         self.out_offs = out_offs
 
-    def run(self, marks=None):
+    def run(self, marks=None, check_device: bool = True):
         L, P, hs = lib(), self.plan.h, stream_handle()
         self.peaks.zero_()
         if marks:
@@ -757,7 +846,13 @@ class StaticEqPipeline:
                                  ptr(self.y), ptr(self.peaks), hs), "stft_ola")
         if marks:
             marks[1].record()
+        if check_device:
+            self.finish()
         return self.result()
+
+    def finish(self) -> int:
+        # no limiter in this pass: only the exchange-barrier check applies
+        return finish_plan(self.plan, None, "StaticEqPipeline")
 
     def result(self) -> Result:
         st = list(self.plan.streams)[:self.ss.n_streams]
@@ -861,6 +956,6 @@ def _minhold_states(levels, tlhs, hyst_db, mh, target):
     return out
 
 
-__all__ = ["StreamSet", "Plan", "GatePipeline", "AdaptivePipeline", "AdaptiveGroups", "StaticEqPipeline",
+__all__ = ["StreamSet", "Plan", "DeviceCheckError", "finish_plan", "GatePipeline", "AdaptivePipeline", "AdaptiveGroups", "StaticEqPipeline",
            "Result", "merge_results", "scale_copy", "frame_r", "compute_frame_levels", "simulate_gate",
            "find_optimal_threshold"]

@@ -246,14 +246,29 @@ def encode_flac_device(y, n: int, ch: int, sr: int, bps: int = 24, timer=None) -
 def write_device(out_path: str, y, n: int, ch: int, sr: int, log=print, timer=None):
     """FLAC PCM_24 of device samples y [n*ch], else the reference's WAV fallback
     at ``out_path.replace('.flac', '.wav')`` (src/process_tomatis.py:242-251).
+    As in the reference, only a failure to *open* the FLAC output (the file or
+    the encoder) falls back to WAV; an error while encoding or writing (a device
+    error in the quantiser, a full disk) removes the partial file and raises.
     Frame bytes are written by a writer thread while later segments encode;
     the header goes over a placeholder at the end.  Returns (written_path, is_flac)."""
     if audio_io.have_soundfile():
         return audio_io.write_with_fallback(out_path, y.cpu().numpy().reshape(n, ch), sr, log=log)
     import queue
     import threading
+    h = _flac()
     try:
-        with open(out_path, "wb") as f:
+        enc = C.c_void_p()
+        _err(h.tomatis_flac_enc_open(ch, sr, 24, C.byref(enc)), "FLAC encoder")
+        h.tomatis_flac_enc_close(enc)
+        f = open(out_path, "wb")
+    except Exception as e:
+        log(f"[WARN] FLAC 写入失败: {e}")
+        wav_path = out_path.replace(".flac", ".wav")
+        audio_io.write(wav_path, y.cpu().numpy().reshape(n, ch), sr, "WAV", "PCM_24")
+        log("[OK] 输出格式: WAV 24-bit (稍后需转换为 FLAC)")
+        return wav_path, False
+    try:
+        with f:
             f.write(b"\0" * 42)
             q = queue.Queue(maxsize=4)
             err = []
@@ -283,16 +298,16 @@ def write_device(out_path: str, y, n: int, ch: int, sr: int, log=print, timer=No
             t0 = time.perf_counter()
             f.seek(0)
             f.write(hdr)
-        if timer is not None:
-            timer.add("write", t0)
-        log("[OK] 输出格式: FLAC 24-bit")
-        return out_path, True
-    except Exception as e:
-        log(f"[WARN] FLAC 写入失败: {e}")
-        wav_path = out_path.replace(".flac", ".wav")
-        audio_io.write(wav_path, y.cpu().numpy().reshape(n, ch), sr, "WAV", "PCM_24")
-        log("[OK] 输出格式: WAV 24-bit (稍后需转换为 FLAC)")
-        return wav_path, False
+    except BaseException:
+        try:
+            os.remove(out_path)
+        except OSError:
+            pass
+        raise
+    if timer is not None:
+        timer.add("write", t0)
+    log("[OK] 输出格式: FLAC 24-bit")
+    return out_path, True
 
 
 def device_stream_set(x, n: int, ch: int, sr: int):
