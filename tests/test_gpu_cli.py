@@ -119,16 +119,32 @@ def test_layer2_cli_gain_protect(tmp_path):
     eq = str(tmp_path / "eq.csv")
     open(eq, "w").write(eq_csv_rows())
     out = str(tmp_path / "l2.flac")
-    layer2_apply_eq.main(["-i", inp, "-o", out, "--eq_csv", eq, "--n_fft", "2048", "--hop", "512"])
+    # FLAC in: the device file path end to end (fileio ingest and egress)
+    inp_flac = str(tmp_path / "in.flac")
+    audio_io.write(inp_flac, x, sr, "FLAC", "PCM_24")
+    layer2_apply_eq.main(["-i", inp_flac, "-o", out, "--eq_csv", eq, "--n_fft", "2048",
+                          "--hop", "512"])
     fr, db = parse_eq_csv(eq_csv_rows())
-    ref = orc.apply_eq_stft(x, sr, fr, db, n_fft=2048, hop=512)
+    xq, _ = audio_io.read(inp_flac)
+    ref = orc.apply_eq_stft(xq, sr, fr, db, n_fft=2048, hop=512)
     y, _ = audio_io.read(_written(out))
     assert y.shape == ref["y"].shape
     # PCM_24 clips the reference's ill-conditioned head samples (F7): compare the rest
     m = (ref["wsum"] >= 1e-3)[:, None] & (np.abs(ref["y"]) < 0.99)
     _cmp(y, ref["y"], m)
-    if ref["y_gp"] is not None:
-        assert os.path.exists(_written(out.replace(".flac", "_gp.flac")))
+    # gain protect: the reference re-reads its PCM_24 output and writes
+    # float32(x * scale) as PCM_24 (src/layer2_apply_eq.py:220-231); bit-exact
+    # given the device's peak
+    r = layer2_apply_eq.apply_eq_stft(inp_flac, str(tmp_path / "l2b.flac"), eq, n_fft=2048,
+                                      hop=512)
+    assert r["peak_seen"] > 0.99, "the case is meant to engage gain protection"
+    scale = np.float32(0.99 / max(r["peak_seen"], 1e-12))
+    y2, _ = audio_io.read(str(tmp_path / "l2b.flac"))
+    np.testing.assert_array_equal(y2, y)
+    gp, _ = audio_io.read(str(tmp_path / "l2b_gp.flac"))
+    v = np.clip(np.rint((y2 * scale).astype(np.float32).astype(np.float64) * 8388607.0),
+                -8388608, 8388607)
+    np.testing.assert_array_equal(gp, (v / 8388608.0).astype(np.float32))
 
 
 def test_batch_runner_single_process(tmp_path):

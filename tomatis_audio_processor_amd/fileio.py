@@ -310,10 +310,25 @@ def write_device(out_path: str, y, n: int, ch: int, sr: int, log=print, timer=No
     return out_path, True
 
 
+def requantize_device(y, n: int, ch: int, bps: int = 24):
+    """Device float32 samples as a PCM_``bps`` file written from y reads back
+    (libsndfile's float -> int rule, then int / 2^(bps-1)): the input of the
+    reference's second pass over its own output (src/layer2_apply_eq.py:220-231)."""
+    torch = _torch()
+    yi = torch.empty(max(1, n * ch), dtype=torch.int32, device="cuda")
+    check(lib().tomatis_float_to_pcm(ptr(y), n * ch, bps, ptr(yi), stream_handle()),
+          "float_to_pcm")
+    out = torch.empty(max(1, n * ch), dtype=torch.float32, device="cuda")
+    check(lib().tomatis_pcm_to_float(ptr(yi), n * ch, bps, ptr(out), stream_handle()),
+          "pcm_to_float")
+    return out[:n * ch]
+
+
 def device_stream_set(x, n: int, ch: int, sr: int):
     """One-stream ``engine.StreamSet`` over a device buffer from read_device."""
     from . import engine
     return engine.StreamSet(x=x, offs=[0], lens=[n], ch=ch, sr=sr)
 
 
-__all__ = ["read_device", "write_device", "encode_flac_device", "device_stream_set", "Timer"]
+__all__ = ["read_device", "write_device", "encode_flac_device", "requantize_device",
+           "device_stream_set", "Timer"]

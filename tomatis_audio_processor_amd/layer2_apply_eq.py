@@ -2,11 +2,12 @@
 src/layer2_apply_eq.py (``load_eq_csv`` :11-46, ``build_gain_per_bin`` :48-64,
 ``apply_eq_stft`` :66-237, CLI :239-263).
 
-One static gain row per file through the same fused kernel; the head pad is
-kept in the output (padded coordinates), and gain protection writes a
-``*_gp.flac`` copy scaled by ``peak_target / peak`` when the output peak
-exceeds ``peak_target``.  The reference scales the PCM_24 re-read of its own
-output; this build scales the float output (<= 1 LSB of 24-bit difference).
+One static gain row per file through the same fused kernel, on the device
+file path (``fileio``: FLAC bytes -> HBM -> FLAC); the head pad is kept in the
+output (padded coordinates), and gain protection writes a ``*_gp.flac`` copy
+scaled by ``peak_target / peak`` when the output peak exceeds ``peak_target``:
+like the reference, the copy scales the PCM_24 samples of the main output
+(re-quantised on the device instead of re-read from the file).
 """
 from __future__ import annotations
 
@@ -14,7 +15,7 @@ import argparse
 
 import numpy as np
 
-from . import audio_io, dsp
+from . import audio_io, dsp  # noqa: F401  (audio_io: format probe)
 
 EPS = dsp.EPS
 load_eq_csv = dsp.load_eq_csv
@@ -37,7 +38,7 @@ def apply_eq_stft(
     peak_target=0.99,
     allow_any_format=False,
 ):
-    from . import engine
+    from . import engine, fileio
     import torch
     sr, ch, _ = audio_io.info(in_path)
     if not allow_any_format:
@@ -45,27 +46,30 @@ def apply_eq_stft(
             raise ValueError(f"期望 48kHz，实际 {sr}")
         if ch != 2:
             raise ValueError(f"期望双声道，实际 {ch}")
-    x, sr = audio_io.read(in_path)
+    # the device file path: FLAC bytes -> HBM, the fused STFT/OLA, HBM -> FLAC
+    x, n, ch, sr = fileio.read_device(in_path)
     eq_freqs, eq_db = load_eq_csv(eq_csv)
     gain_bins = build_gain_per_bin(sr, n_fft, eq_freqs, eq_db)
-    ss = engine.StreamSet.from_arrays([x], sr)
+    ss = fileio.device_stream_set(x, n, ch, sr)
     pipe = engine.StaticEqPipeline(ss, gain_bins, n_fft=n_fft, hop=hop, pad=pad,
                                    global_gain_db=global_gain_db)
     res = pipe.run()
-    torch.cuda.synchronize()
-    y_dev = res.y[:res.out_lens[0] * ch]
-    y = res.output(0)
-    written, is_flac = audio_io.write_with_fallback(out_path, y, sr, log=lambda m: None)
+    n_out = res.out_lens[0]
+    y_dev = res.y[res.out_offs[0]:res.out_offs[0] + n_out * ch]
+    written, is_flac = fileio.write_device(out_path, y_dev, n_out, ch, sr, log=lambda m: None)
     if not is_flac:
         print(f"[WARN] FLAC 写入失败，先写 WAV: {written}")
     peak_seen = float(res.stream_peaks(0)[0])
     if auto_gain_protect and peak_seen > peak_target:
         scale = peak_target / max(peak_seen, EPS)
         print(f"[GAIN_PROTECT] peak={peak_seen:.4f} > {peak_target}, apply scale={scale:.4f}")
-        ygp = engine.scale_copy(y_dev, scale).cpu().numpy().reshape(-1, ch)
+        # the reference re-reads its PCM_24 output and scales that
+        # (src/layer2_apply_eq.py:220-231): the same samples, on the device
+        ygp = engine.scale_copy(fileio.requantize_device(y_dev, n_out, ch, 24), scale)
         tmp_out = out_path.replace(".flac", "_gp.flac")
-        gp_written, _ = audio_io.write_with_fallback(tmp_out, ygp, sr, log=lambda m: None)
+        gp_written, _ = fileio.write_device(tmp_out, ygp, n_out, ch, sr, log=lambda m: None)
         print(f"[DONE] gain-protected file: {gp_written}")
+    torch.cuda.synchronize()
     print("[DONE] EQ applied.")
     if not is_flac:
         print(f"[NOTE] 输出为 WAV: {written}，可用 ffmpeg 转 FLAC。")
