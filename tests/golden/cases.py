@@ -45,6 +45,14 @@ CASES = [
          seed=9, params=dict(gate_ui=50, n_fft=1024, hop=256)),
     dict(name="std_48k_st_8192_2048", mode="standard", sr=S48, ch=2, N=288000 + 8192 + 555,
          seed=10, params=dict(gate_ui=50, n_fft=8192, hop=2048)),
+    # n_fft that is not a power of two (Bluestein) and 16384 (round 3)
+    dict(name="std_48k_st_3000_750", mode="standard", sr=S48, ch=2, N=192000 + 3000 + 91,
+         seed=51, params=dict(gate_ui=50, n_fft=3000, hop=750)),
+    dict(name="std_48k_st_16384_4096", mode="standard", sr=S48, ch=2, N=288000 + 16384 + 313,
+         seed=52, params=dict(gate_ui=50, n_fft=16384, hop=4096)),
+    dict(name="xfade_48k_st_2400_600", mode="xfade", sr=S48, ch=2, N=144000 + 2400 + 7,
+         seed=54, params=dict(gate_ui=50, gate_offset=-90, n_fft=2400, hop=600,
+                              xfade_ms=200.0)),
     # --- xfade (src/process_tomatis_xfade.py) ------------------------------
     dict(name="xfade_48k_st_2048_512_500ms", mode="xfade", sr=S48, ch=2,
          N=288000 + 5000, seed=11,
@@ -67,6 +75,12 @@ CASES = [
     # the adaptive processor takes any channel count (no guard, adaptive.py:179-183)
     dict(name="adapt_48k_4ch_2048_512", mode="adaptive", sr=S48, ch=4, N=48000 * 5 + 321,
          seed=24, params=dict(n_fft=2048, hop=512)),
+    # more channels than the L + iR register path (round 3: 10 channels, and a
+    # prime n_fft on the adaptive path)
+    dict(name="adapt_48k_10ch_2048_512", mode="adaptive", sr=S48, ch=10, N=48000 * 3 + 77,
+         seed=53, params=dict(n_fft=2048, hop=512)),
+    dict(name="adapt_44k_st_1999_500", mode="adaptive", sr=S44, ch=2, N=44100 * 4 + 5,
+         seed=55, params=dict(n_fft=1999, hop=500)),
     dict(name="adapt_44k_st_512_128", mode="adaptive", sr=S44, ch=2, N=44100 * 4 + 99,
          seed=25, params=dict(n_fft=512, hop=128)),
     # --- layer 2 (src/layer2_apply_eq.py) -----------------------------------

@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <complex>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -50,29 +51,36 @@ struct GateSeg {      // gate segment
 // Levels: r = sqrt(mean(m*m) + EPS), m = sqrt(mean_c(x_c^2)), numpy pairwise
 // ===========================================================================
 template <typename T>
-__device__ __forceinline__ T msq_of(const float* xs, int ch, T scale);
-
-template <>
-__device__ __forceinline__ float msq_of<float>(const float* xs, int ch, float scale) {
-  // frame**2 -> mean over channels (sequential from 0, n<8 pairwise branch) -> sqrt -> square
-  float acc = 0.f;
-  for (int c = 0; c < ch; ++c) {
-    const float v = xs[c] * scale;
-    acc = acc + v * v;
-  }
-  const float mean = (ch == 1) ? acc : ((ch == 2) ? acc * 0.5f : acc / (float)ch);
-  const float m = sqrtf(mean);
-  return m * m;
+__device__ __forceinline__ T sq_ch(const float* xs, int c, T scale) {
+  const T v = (T)xs[c] * scale;
+  return v * v;
 }
-template <>
-__device__ __forceinline__ double msq_of<double>(const float* xs, int ch, double scale) {
-  double acc = 0.0;
-  for (int c = 0; c < ch; ++c) {
-    const double v = (double)xs[c] * scale;
-    acc = acc + v * v;
+
+// frame**2 -> mean over channels -> sqrt -> square.  numpy reduces the channel
+// axis with its pairwise sum: sequential from 0 below 8 channels, otherwise 8
+// accumulators, the fixed tree and a sequential remainder (plan: ch <= 128).
+template <typename T>
+__device__ __forceinline__ T msq_of(const float* xs, int ch, T scale) {
+  T acc;
+  if (ch < 8) {
+    acc = (T)0;
+    for (int c = 0; c < ch; ++c) acc = acc + sq_ch<T>(xs, c, scale);
+  } else {
+    T r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = sq_ch<T>(xs, j, scale);
+    int i = 8;
+    for (; i < ch - (ch % 8); i += 8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = r[j] + sq_ch<T>(xs, i + j, scale);
+    }
+    acc = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < ch; ++i) acc = acc + sq_ch<T>(xs, i, scale);
   }
-  const double mean = (ch == 1) ? acc : ((ch == 2) ? acc * 0.5 : acc / (double)ch);
-  const double m = sqrt(mean);
+  const T mean = (ch == 1) ? acc : ((ch == 2) ? acc * (T)0.5 : acc / (T)ch);
+  T m;
+  if constexpr (sizeof(T) == 4) m = sqrtf(mean);
+  else m = sqrt(mean);
   return m * m;
 }
 
@@ -152,6 +160,85 @@ __global__ __launch_bounds__(256) void k_levels(const float* __restrict__ x,
     const T mean = sum / (T)n_fft;
     const T r = sqrt(mean + (T)(sizeof(T) == 4 ? (double)kEps32 : kEps64));
     r_out[S.frame_base + blk.k0 + threadIdx.x] = r;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Levels for any n_fft (not a power of two in [256, 8192], or a frame larger
+// than the block LDS): numpy's pairwise_sum(a, n) splits at n2 = n/2 - (n/2)%8
+// until n <= 128, so its tree over a frame is fixed by n alone.  The host
+// records the leaves (offset, length) and the combination order as a postfix
+// program (leaf index >= 0 pushes that leaf's sum, -1 adds the top two).  One
+// block per frame: threads sum leaves straight from HBM (numpy's block rule:
+// sequential below 8, else 8 accumulators + tree + sequential remainder), one
+// thread runs the program.
+// ---------------------------------------------------------------------------
+constexpr int kPwMaxLeaves = 2048;
+
+template <typename T>
+__device__ T pw_leaf(const float* xs, int64_t n, int ch, int64_t p0, int len, T scale) {
+  auto m2 = [&](int i) -> T {
+    const int64_t p = p0 + i;
+    return (p >= 0 && p < n) ? msq_of<T>(xs + p * ch, ch, scale) : (T)0;
+  };
+  if (len < 8) {
+    T acc = (T)0;
+    for (int i = 0; i < len; ++i) acc = acc + m2(i);
+    return acc;
+  }
+  T r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = m2(j);
+  int i = 8;
+  for (; i < len - (len % 8); i += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = r[j] + m2(i + j);
+  }
+  T res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < len; ++i) res = res + m2(i);
+  return res;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_levels_any(const float* __restrict__ x,
+                                                    const TomatisStream* __restrict__ st,
+                                                    int n_streams, int n_fft, int hop, int ch,
+                                                    const int2* __restrict__ leaf, int n_leaf,
+                                                    const int16_t* __restrict__ prog, int n_prog,
+                                                    int64_t total_frames, T* __restrict__ r_out) {
+  __shared__ T ls[kPwMaxLeaves];
+  for (int64_t f = blockIdx.x; f < total_frames; f += gridDim.x) {
+    int lo = 0, hi = n_streams - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (st[mid].frame_base <= f) lo = mid;
+      else hi = mid - 1;
+    }
+    const TomatisStream S = st[lo];
+    const int64_t s_k = S.first_start + (f - S.frame_base) * hop;
+    const float* xs = x + S.in_off;
+    const T scale = (T)S.in_scale;
+    for (int l = threadIdx.x; l < n_leaf; l += blockDim.x) {
+      const int2 lf = leaf[l];
+      ls[l] = pw_leaf<T>(xs, S.n, ch, s_k + lf.x, lf.y, scale);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      T stk[40];
+      int sp = 0;
+      for (int i = 0; i < n_prog; ++i) {
+        const int op = prog[i];
+        if (op >= 0) {
+          stk[sp++] = ls[op];
+        } else {
+          const T b = stk[--sp];
+          stk[sp - 1] = stk[sp - 1] + b;
+        }
+      }
+      const T mean = stk[0] / (T)n_fft;
+      r_out[f] = sqrt(mean + (T)(sizeof(T) == 4 ? (double)kEps32 : kEps64));
+    }
+    __syncthreads();
   }
 }
 
@@ -1271,6 +1358,18 @@ struct tomatis_plan_s {
   int64_t* grp_base = nullptr;
   int64_t* leaf_base = nullptr;
   void* leaves = nullptr;
+  // levels for any n_fft (k_levels_any): numpy pairwise leaves + postfix program
+  bool lvl_any = false;
+  int2* pw_leaf = nullptr;
+  int16_t* pw_prog = nullptr;
+  int n_pw_leaf = 0, n_pw_prog = 0;
+  // any-size transform: FFT length M (= n_fft, or Bluestein's power of two)
+  int lds_M = 0;
+  bool blue = false;
+  float2* blue_b = nullptr;   // chirp exp(i pi n^2 / N), n < N
+  float2* blue_h = nullptr;   // FFT_M of the chirp filter / M
+  float2* glb_work = nullptr; // M > kLdsMaxM: per-block ping-pong buffers in HBM
+  int glb_blocks = 0;
 };
 
 namespace {
@@ -1327,7 +1426,8 @@ int tomatis_plan_destroy(tomatis_plan_t p) {
                   p->pos_base, p->chunks, p->mh_tf, p->mh_cnt, p->mh_off, p->mh_sym, p->mh_soff, p->gperm,
                   p->grp_base, p->leaf_base, p->leaves, p->gsum, p->gcarry, p->gcarry_in,
                   p->aq, p->afin, p->acin,
-                  p->chunk_need, p->chunk_done, p->chunk_rng, p->err, p->twL};
+                  p->chunk_need, p->chunk_done, p->chunk_rng, p->err, p->twL,
+                  p->pw_leaf, p->pw_prog, p->blue_b, p->blue_h, p->glb_work};
   for (void* q : ptrs) dfree(q);
   delete p;
   return TOMATIS_OK;
@@ -1352,6 +1452,42 @@ static bool gate_exclusive(const TomatisStream& S) {
   for (int i = 0; i < S.n_off_exc; ++i)
     if (on(S.off_exc[i]) && off(S.off_exc[i])) return false;
   return true;
+}
+
+// in-place iterative radix-2 FFT in double (plan set-up: Bluestein filter)
+static void fft_host(std::vector<std::complex<double>>& a) {
+  const size_t n = a.size();
+  for (size_t i = 1, j = 0; i < n; ++i) {
+    size_t bit = n >> 1;
+    for (; j & bit; bit >>= 1) j ^= bit;
+    j ^= bit;
+    if (i < j) std::swap(a[i], a[j]);
+  }
+  for (size_t len = 2; len <= n; len <<= 1) {
+    for (size_t i = 0; i < n; i += len)
+      for (size_t k = 0; k < len / 2; ++k) {
+        const std::complex<double> w = std::polar(1.0, -2.0 * M_PI * (double)k / (double)len);
+        const std::complex<double> u = a[i + k], v = a[i + k + len / 2] * w;
+        a[i + k] = u + v;
+        a[i + k + len / 2] = u - v;
+      }
+  }
+}
+
+// numpy pairwise_sum's tree over n elements at offset off (loops_utils.h.src:
+// blocks of <= 128, split at n/2 rounded down to a multiple of 8): leaves in
+// order, and the postfix combination program
+static void pw_build(int off, int n, std::vector<int2>& lv, std::vector<int16_t>& prog) {
+  if (n <= 128) {
+    prog.push_back((int16_t)lv.size());
+    lv.push_back(make_int2(off, n));
+    return;
+  }
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  pw_build(off, n2, lv, prog);
+  pw_build(off + n2, n - n2, lv, prog);
+  prog.push_back(-1);
 }
 
 static int plan_build(tomatis_plan_s* p, const float* window) {
@@ -1464,8 +1600,28 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
   }
   p->n_runs = (int)runs.size();
   if ((rc = dalloc_copy(&p->runs, runs))) return rc;
-  // --- levels blocks ---
+  // --- levels: any n_fft (numpy pairwise program) ---
+  // k_levels holds a block's span in LDS (f64: half as many samples); frames
+  // that do not fit, and every n_fft that is not a power of two >= 256, take
+  // k_levels_any
   {
+    const bool pow2 = (N & (N - 1)) == 0;
+    const int cap32 = ((kLevelLds + 256) * 128) / 132 - 8;
+    const int cap64 = ((kLevelLds / 2 + 256) * 128) / 132 - 8;
+    p->lvl_any = !pow2 || N < 256 || N > cap32;
+    if (p->lvl_any || N > cap64) {
+      std::vector<int2> lv;
+      std::vector<int16_t> prog;
+      pw_build(0, N, lv, prog);
+      if ((int)lv.size() > kPwMaxLeaves) return TOMATIS_E_UNSUPPORTED;
+      p->n_pw_leaf = (int)lv.size();
+      p->n_pw_prog = (int)prog.size();
+      if ((rc = dalloc_copy(&p->pw_leaf, lv))) return rc;
+      if ((rc = dalloc_copy(&p->pw_prog, prog))) return rc;
+    }
+  }
+  // --- levels blocks ---
+  if (!p->lvl_any) {
     const int arr_f32 = kLevelLds + 256;  // matches k_levels<float> LDS
     const int cap = (arr_f32 * 128) / 132 - 8;
     p->lvl_nf = std::max(1, (cap - N) / hop + 1);
@@ -1550,38 +1706,65 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
       winv[m] = 1.0f / den;
     }
     p->rmax = (N + hop - 1) / hop;
-    const int NRr = p->NR;
-    // scaled-DIF output scales of the register FFT (tm_common.h): the step-2
-    // table absorbs the forward NR-point DFT's, the synthesis window the
-    // inverse's (whose inputs carry 1 / the forward's)
-    const double* sigF = NRr == 32 ? splan<32, 0>().sig : splan<16, 0>().sig;
-    const double* sigI = NRr == 32 ? splan<32, 2>().sig : splan<16, 2>().sig;
-    std::vector<cf> twN((size_t)NRr * P), twP(P);
-    for (int k2 = 0; k2 < NRr; ++k2)
-      for (int n1 = 0; n1 < P; ++n1) {
-        const double ang = -2.0 * M_PI * (double)((int64_t)n1 * k2 % N) / (double)N;
-        twN[((size_t)(k2 >> 1) * P + n1) * 2 + (k2 & 1)] = {(float)(cos(ang) * sigF[k2]),
-                                                           (float)(sin(ang) * sigF[k2])};
+    if (!p->lds) {  // register kernels only (NR = 16 or 32)
+      const int NRr = p->NR;
+      // scaled-DIF output scales of the register FFT (tm_common.h): the step-2
+      // table absorbs the forward NR-point DFT's, the synthesis window the
+      // inverse's (whose inputs carry 1 / the forward's)
+      const double* sigF = NRr == 32 ? splan<32, 0>().sig : splan<16, 0>().sig;
+      const double* sigI = NRr == 32 ? splan<32, 2>().sig : splan<16, 2>().sig;
+      std::vector<cf> twN((size_t)NRr * P), twP(P);
+      for (int k2 = 0; k2 < NRr; ++k2)
+        for (int n1 = 0; n1 < P; ++n1) {
+          const double ang = -2.0 * M_PI * (double)((int64_t)n1 * k2 % N) / (double)N;
+          twN[((size_t)(k2 >> 1) * P + n1) * 2 + (k2 & 1)] = {(float)(cos(ang) * sigF[k2]),
+                                                             (float)(sin(ang) * sigF[k2])};
+        }
+      std::vector<float> winS(N);
+      for (int t = 0; t < N; ++t) winS[t] = (float)((double)w[t] * sigI[t / P]);
+      for (int m = 0; m < P; ++m) {
+        const double ang = -2.0 * M_PI * (double)m / (double)P;
+        twP[m] = {(float)cos(ang), (float)sin(ang)};
       }
-    std::vector<float> winS(N);
-    for (int t = 0; t < N; ++t) winS[t] = (float)((double)w[t] * sigI[t / P]);
-    for (int m = 0; m < P; ++m) {
-      const double ang = -2.0 * M_PI * (double)m / (double)P;
-      twP[m] = {(float)cos(ang), (float)sin(ang)};
+      if ((rc = dalloc_copy(&p->winS, winS))) return rc;
+      if ((rc = dalloc_copy(&p->twN, twN))) return rc;
+      if ((rc = dalloc_copy(&p->twP, twP))) return rc;
     }
     if ((rc = dalloc_copy(&p->win, w))) return rc;
-    if ((rc = dalloc_copy(&p->winS, winS))) return rc;
     if ((rc = dalloc_copy(&p->win2, w2))) return rc;
     if ((rc = dalloc_copy(&p->winv, winv))) return rc;
-    if ((rc = dalloc_copy(&p->twN, twN))) return rc;
-    if ((rc = dalloc_copy(&p->twP, twP))) return rc;
     if (p->lds) {
-      std::vector<float2> tl(N);
-      for (int t = 0; t < N; ++t) {
-        const double ang = -2.0 * M_PI * (double)t / (double)N;
+      const int M = p->lds_M;
+      std::vector<float2> tl(M);
+      for (int t = 0; t < M; ++t) {
+        const double ang = -2.0 * M_PI * (double)t / (double)M;
         tl[t] = make_float2((float)cos(ang), (float)sin(ang));
       }
       if ((rc = dalloc_copy(&p->twL, tl))) return rc;
+      if (p->blue) {
+        // chirp b_n = exp(i pi n^2 / N): n^2 mod 2N exact in integers
+        std::vector<std::complex<double>> bd(N), h(M, 0.0);
+        std::vector<float2> bf(N), hf(M);
+        for (int n = 0; n < N; ++n) {
+          const int64_t q = ((int64_t)n * n) % (2 * (int64_t)N);
+          bd[n] = std::polar(1.0, M_PI * (double)q / (double)N);
+          bf[n] = make_float2((float)bd[n].real(), (float)bd[n].imag());
+        }
+        for (int n = 0; n < N; ++n) h[n] = bd[n];
+        for (int n = 1; n < N; ++n) h[M - n] = bd[n];
+        fft_host(h);
+        for (int k = 0; k < M; ++k)
+          hf[k] = make_float2((float)(h[k].real() / M), (float)(h[k].imag() / M));
+        if ((rc = dalloc_copy(&p->blue_b, bf))) return rc;
+        if ((rc = dalloc_copy(&p->blue_h, hf))) return rc;
+      }
+      if (M > kLdsMaxM && p->total_frames > 0) {
+        const int64_t items = p->total_frames * ((d.ch + 1) / 2);
+        p->glb_blocks = (int)std::min<int64_t>(items, 512);
+        if (hipMalloc(reinterpret_cast<void**>(&p->glb_work),
+                      (size_t)p->glb_blocks * 2 * M * sizeof(float2)))
+          return TOMATIS_E_NOMEM;
+      }
     }
   }
   // --- limiter chunk descriptors, output prefix ---
@@ -1700,8 +1883,8 @@ int tomatis_plan_create(tomatis_plan_t* out, const TomatisPlanDesc* desc, const 
   if (!out || !desc || !window || (!streams && n_streams > 0) || n_streams < 0) return TOMATIS_E_ARG;
   *out = nullptr;
   const TomatisPlanDesc d = *desc;
-  if (d.n_fft < 256 || d.n_fft > 8192 || (d.n_fft & (d.n_fft - 1))) return TOMATIS_E_UNSUPPORTED;
-  if (d.ch < 1 || d.ch > 8) return TOMATIS_E_UNSUPPORTED;
+  if (d.n_fft < 2 || d.n_fft > kMaxNfft) return TOMATIS_E_UNSUPPORTED;
+  if (d.ch < 1 || d.ch > kMaxCh) return TOMATIS_E_UNSUPPORTED;
   if (d.hop < 1 || d.hop > d.n_fft) return TOMATIS_E_ARG;
   if (d.up_delay_frames < 0 || d.up_delay_frames + 2 > kMaxGateStates) return TOMATIS_E_UNSUPPORTED;
   if (d.min_hold_frames < 0 || 2 * (d.min_hold_frames + 1) > 65535) return TOMATIS_E_UNSUPPORTED;
@@ -1715,8 +1898,15 @@ int tomatis_plan_create(tomatis_plan_t* out, const TomatisPlanDesc* desc, const 
   // n_fft 2048: one wave per frame (P = 64, 32 registers, wave-local exchanges)
   // unless TOMATIS_P64=0; otherwise two waves per frame (P = 128)
   // register kernels: n_fft 2048 / 4096 with <= 2 channels (L + iR); every
-  // other power of two in [256, 8192] or more channels: the any-size LDS path
+  // other n_fft or more channels: the any-size path (Stockham FFT of length M,
+  // Bluestein when n_fft is not a power of two)
   p->lds = !(N == 2048 || N == 4096) || d.ch > 2 || env_int("TOMATIS_FORCE_LDS", 0) != 0;
+  if (p->lds) {
+    p->blue = (N & (N - 1)) != 0;
+    int M = 1;
+    while (M < (p->blue ? 2 * N - 1 : N)) M <<= 1;
+    p->lds_M = M;
+  }
   p->P = p->lds ? 64 : ((N == 2048 && env_int("TOMATIS_P64", 1)) ? 64 : 128);
   p->NR = N / p->P;
   p->SH = (!p->lds && hop % p->P == 0) ? hop / p->P : 0;
@@ -1783,8 +1973,22 @@ int tomatis_plan_update_streams(tomatis_plan_t p, const TomatisStream* streams, 
 
 int tomatis_levels(tomatis_plan_t p, const float* x, void* r_out, int32_t prec, void* hs) {
   if (!p || !x || !r_out) return TOMATIS_E_ARG;
-  if (p->n_lblocks == 0) return TOMATIS_OK;
+  if (p->total_frames == 0) return TOMATIS_OK;
   hipStream_t s = (hipStream_t)hs;
+  const bool any = p->lvl_any || (prec == TOMATIS_F64 && p->n_pw_prog > 0);
+  if (any && (prec == TOMATIS_F32 || prec == TOMATIS_F64)) {
+    const unsigned g = (unsigned)std::min<int64_t>(p->total_frames, 1 << 16);
+    if (g == 0) return TOMATIS_OK;
+    if (prec == TOMATIS_F32)
+      hipLaunchKernelGGL(k_levels_any<float>, dim3(g), dim3(256), 0, s, x, p->st, p->n_streams,
+                         p->d.n_fft, p->d.hop, p->d.ch, p->pw_leaf, p->n_pw_leaf, p->pw_prog,
+                         p->n_pw_prog, p->total_frames, (float*)r_out);
+    else
+      hipLaunchKernelGGL(k_levels_any<double>, dim3(g), dim3(256), 0, s, x, p->st, p->n_streams,
+                         p->d.n_fft, p->d.hop, p->d.ch, p->pw_leaf, p->n_pw_leaf, p->pw_prog,
+                         p->n_pw_prog, p->total_frames, (double*)r_out);
+    return launch_check();
+  }
   if (p->leaf_path && (prec == TOMATIS_F32 || prec == TOMATIS_F64)) {
     const unsigned gblk = (unsigned)((p->n_groups + 3) / 4);
     const unsigned fblk = (unsigned)((p->total_frames + 255) / 256);
@@ -2012,6 +2216,12 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
     L.win = p->win;
     L.win2 = p->win2;
     L.tw = p->twL;
+    L.blue_b = p->blue_b;
+    L.blue_h = p->blue_h;
+    L.work = p->glb_work;
+    L.M = p->lds_M;
+    L.blue = p->blue ? 1 : 0;
+    L.work_blocks = p->glb_blocks;
     L.scratch = reinterpret_cast<float*>(p->scratch);
     L.y = y;
     L.peaks = peaks;

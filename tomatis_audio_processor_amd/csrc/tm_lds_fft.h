@@ -20,7 +20,7 @@ __device__ __forceinline__ void lds_fft(float2* __restrict__ buf, const float2* 
   constexpr int n = N;
   constexpr int logn = __builtin_ctz(N);
   constexpr int kMaxU2 = (N / 2 + kT - 1) / kT;  // radix-2 butterflies per thread
-  constexpr int kMaxU4 = (N / 4 + kT - 1) / kT;  // radix-4 butterflies per thread
+  constexpr int kMaxU4 = (N / 4 + kT - 1) / kT > 0 ? (N / 4 + kT - 1) / kT : 1;  // radix-4 per thread
   const int t = threadIdx.x;
   int Ns = 1;
   if constexpr (logn & 1) {  // radix-2 stage at Ns = 1: out[2j + q] = a +- b

@@ -59,9 +59,14 @@ struct MainArgs {
   unsigned long long* prof;  // TM_PROFILE builds only: per-phase wave cycles
 };
 
-// Any-size path (n_fft a power of two in [256, 8192], any hop, 1..8 channels):
-// per (frame, channel pair) an LDS Stockham FFT, windowed frames to scratch
-// float [frame][n_fft][ch], then a per-position gather in frame order.
+// Any-size path (any n_fft in [2, kMaxNfft], any hop, 1..kMaxCh channels): per
+// (frame, channel pair) a Stockham FFT of length M (n_fft when it is a power
+// of two, else Bluestein's power of two >= 2 n_fft - 1) in LDS (M <= kLdsMaxM)
+// or in per-block HBM buffers, windowed frames to scratch float
+// [frame][n_fft][ch], then a per-position gather in frame order.
+constexpr int kMaxNfft = 1 << 16;
+constexpr int kMaxCh = 128;
+constexpr int kLdsMaxM = 16384;
 struct LdsArgs {
   const float* x;
   const TomatisStream* st;
@@ -70,13 +75,17 @@ struct LdsArgs {
   const uint16_t* rows;
   const float* win;     // [N]
   const float* win2;    // [N]
-  const float2* tw;     // [N] exp(-2 pi i t / N)
+  const float2* tw;     // [M] exp(-2 pi i t / M)
+  const float2* blue_b; // Bluestein: [N] chirp exp(i pi n^2 / N)
+  const float2* blue_h; // Bluestein: [M] FFT_M(chirp filter) / M
+  float2* work;         // M > kLdsMaxM: [gridDim.x][2][M] per-block buffers
   float* scratch;       // [total_frames][N][ch]
   float* y;
   uint32_t* peaks;
   const int64_t* pos_base;  // output position prefix per stream
   int64_t total_frames, total_out;
   int n_fft, hop, ch, n_bins, norm_mode;
+  int M, blue, work_blocks;
 };
 void launch_lds_frames(const LdsArgs& A, hipStream_t s);
 void launch_lds_gather(const LdsArgs& A, hipStream_t s);

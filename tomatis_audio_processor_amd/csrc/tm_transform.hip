@@ -728,13 +728,20 @@ __global__ __launch_bounds__(256) void k_ola_gather(MainArgs A, int n_streams,
 
 
 // ---------------------------------------------------------------------------
-// Any-size path: n_fft a power of two in [256, 8192], any hop, 1..8 channels
-// (the register kernels above cover n_fft 2048 / 4096 with <= 2 channels).
+// Any-size path: any n_fft in [2, 65536], any hop, 1..128 channels (the
+// register kernels above cover n_fft 2048 / 4096 with <= 2 channels).
 // Reference: the same per-frame filter, src/process_tomatis.py:394-406 (and the
-// adaptive :298-327 / layer2 :155-198 copies).  Workgroup = (frame, channel
-// pair c0, c1): frame of (x*in_scale)*win packed as c0 + i c1, forward FFT in
-// LDS, real even gain row (1/N folded in), inverse as conj(FFT(conj(.))),
-// synthesis window, to scratch; the OLA is a per-position gather below.
+// adaptive :298-327 / layer2 :155-198 copies), whose np.fft.rfft / irfft take
+// any length.  Work item = (frame, channel pair c0, c1): frame of
+// (x*in_scale)*win packed as c0 + i c1, forward DFT, real even gain row (1/N
+// folded in), inverse as conj(DFT(conj(.))), synthesis window, to scratch; the
+// OLA is a per-position gather below.  The DFT is a Stockham FFT of length
+// M = n_fft when n_fft is a power of two, otherwise Bluestein's chirp-z form
+// over M = 2^k >= 2 n_fft - 1:
+//   X[k] = conj(b_k) * IFFT_M(FFT_M(z * conj(b)) * FFT_M(h))[k],
+//   b_n = exp(i pi n^2 / N), h = b on [0, N) and mirrored at the top of [0, M).
+// M <= 16384 runs in LDS (one workgroup per item); larger M in per-block HBM
+// ping-pong buffers (radix-2 Stockham, workgroup barriers between stages).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int stream_of_frame(const TomatisStream* st, int n, int64_t fg) {
   int lo = 0, hi = n - 1;
@@ -746,51 +753,163 @@ __device__ __forceinline__ int stream_of_frame(const TomatisStream* st, int n, i
   return lo;
 }
 
-template <int N>
-__global__ __launch_bounds__(256) void k_stft_lds(LdsArgs A) {
-  __shared__ float2 buf[N];
-  const int64_t fg = blockIdx.x;
-  const TomatisStream S = A.st[stream_of_frame(A.st, A.n_streams, fg)];
-  const int64_t k = fg - S.frame_base;
-  const int64_t s_k = S.first_start + k * A.hop;
-  const int ch = A.ch, c0 = 2 * blockIdx.y, c1 = c0 + 1;
-  const bool has1 = c1 < ch;
-  const float* xs = A.x + S.in_off;
-  const float isc = S.in_scale;
-  for (int i = threadIdx.x; i < N; i += 256) {
-    const int64_t p = s_k + i;
-    const bool in = p >= 0 && p < S.n;
-    float a = in ? xs[p * ch + c0] : 0.f;
-    float b = (in && has1) ? xs[p * ch + c1] : 0.f;
+__device__ __forceinline__ float2 conjf2(float2 a) { return make_float2(a.x, -a.y); }
+__device__ __forceinline__ float2 cmul_conj(float2 a, float2 b) {  // a * conj(b)
+  return make_float2(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
+}
+
+// forward DFT of buf[0, N) in LDS, in place (callers synchronise before)
+template <int M, bool BLUE>
+__device__ __forceinline__ void lds_dft(float2* buf, const LdsArgs& A) {
+  if constexpr (!BLUE) {
+    tlds::lds_fft<M>(buf, A.tw);
+  } else {
+    const int N = A.n_fft;
+    for (int n = threadIdx.x; n < M; n += blockDim.x)
+      buf[n] = n < N ? cmul_conj(buf[n], A.blue_b[n]) : make_float2(0.f, 0.f);
+    __syncthreads();
+    tlds::lds_fft<M>(buf, A.tw);
+    for (int k = threadIdx.x; k < M; k += blockDim.x)
+      buf[k] = conjf2(tlds::cmul(buf[k], A.blue_h[k]));
+    __syncthreads();
+    tlds::lds_fft<M>(buf, A.tw);
+    for (int k = threadIdx.x; k < N; k += blockDim.x)
+      buf[k] = conjf2(tlds::cmul(buf[k], A.blue_b[k]));
+    __syncthreads();
+  }
+}
+
+// radix-2 Stockham over HBM buffers a -> b -> a ...; returns the buffer holding
+// FFT_m(a) (the workgroup's own buffers; barriers order the stages)
+__device__ float2* glb_fft(float2* a, float2* b, int m, const float2* __restrict__ tw) {
+  const int h = m >> 1;
+  for (int Ns = 1; Ns < m; Ns <<= 1) {
+    const int ts = m / (2 * Ns);
+    for (int j = threadIdx.x; j < h; j += blockDim.x) {
+      const int k = j & (Ns - 1);
+      const float2 v0 = a[j];
+      float2 v1 = a[j + h];
+      if (Ns > 1) v1 = tlds::cmul(v1, tw[k * ts]);
+      const int d = (j - k) * 2 + k;
+      b[d] = tlds::cadd(v0, v1);
+      b[d + Ns] = tlds::csub(v0, v1);
+    }
+    __syncthreads();
+    float2* t = a;
+    a = b;
+    b = t;
+  }
+  return a;
+}
+
+// forward DFT of w0[0, N) (w0, w1: the workgroup's two M-element buffers);
+// returns the buffer holding the result
+__device__ float2* glb_dft(float2* w0, float2* w1, const LdsArgs& A) {
+  const int N = A.n_fft, M = A.M;
+  if (!A.blue) return glb_fft(w0, w1, M, A.tw);
+  for (int n = threadIdx.x; n < M; n += blockDim.x)
+    w0[n] = n < N ? cmul_conj(w0[n], A.blue_b[n]) : make_float2(0.f, 0.f);
+  __syncthreads();
+  float2* r = glb_fft(w0, w1, M, A.tw);
+  for (int k = threadIdx.x; k < M; k += blockDim.x) r[k] = conjf2(tlds::cmul(r[k], A.blue_h[k]));
+  __syncthreads();
+  float2* o = (r == w0) ? w1 : w0;
+  r = glb_fft(r, o, M, A.tw);
+  for (int k = threadIdx.x; k < N; k += blockDim.x) r[k] = conjf2(tlds::cmul(r[k], A.blue_b[k]));
+  __syncthreads();
+  return r;
+}
+
+struct FrameItem {
+  TomatisStream S;
+  int64_t fg, s_k;
+  int c0, c1;
+  bool has1;
+};
+__device__ __forceinline__ FrameItem frame_item(const LdsArgs& A, int64_t fg, int pair) {
+  FrameItem it;
+  it.S = A.st[stream_of_frame(A.st, A.n_streams, fg)];
+  it.fg = fg;
+  it.s_k = it.S.first_start + (fg - it.S.frame_base) * A.hop;
+  it.c0 = 2 * pair;
+  it.c1 = it.c0 + 1;
+  it.has1 = it.c1 < A.ch;
+  return it;
+}
+__device__ __forceinline__ void load_frame(const LdsArgs& A, const FrameItem& it, float2* buf) {
+  const int ch = A.ch, N = A.n_fft;
+  const float* xs = A.x + it.S.in_off;
+  const float isc = it.S.in_scale;
+  for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    const int64_t p = it.s_k + i;
+    const bool in = p >= 0 && p < it.S.n;
+    float a = in ? xs[p * ch + it.c0] : 0.f;
+    float b = (in && it.has1) ? xs[p * ch + it.c1] : 0.f;
     const float w = A.win[i];
     a = (a * isc) * w;  // x * in_scale first, then the window: two roundings as the reference
     b = (b * isc) * w;
     buf[i] = make_float2(a, b);
   }
-  __syncthreads();
-  tlds::lds_fft<N>(buf, A.tw);
-  const uint16_t row = A.rows[S.frame_base + k];
+}
+// spectrum -> conj(X * g / N) for the inverse pass
+__device__ __forceinline__ void apply_gain(const LdsArgs& A, const FrameItem& it, float2* buf) {
+  const int N = A.n_fft;
+  const uint16_t row = A.rows[it.fg];
   const float* g = A.gains + (int64_t)row * A.n_bins;
-  constexpr float inv_n = 1.0f / (float)N;  // exact (power of two)
-  for (int b = threadIdx.x; b < N; b += 256) {
+  const float inv_n = 1.0f / (float)N;
+  for (int b = threadIdx.x; b < N; b += blockDim.x) {
     const float gk = g[b <= N / 2 ? b : N - b] * inv_n;
     const float2 v = buf[b];
-    buf[b] = make_float2(v.x * gk, -(v.y * gk));  // conj for the inverse
+    buf[b] = make_float2(v.x * gk, -(v.y * gk));
   }
-  __syncthreads();
-  tlds::lds_fft<N>(buf, A.tw);
-  float* out = A.scratch + fg * (int64_t)N * ch;
-  for (int i = threadIdx.x; i < N; i += 256) {
+}
+__device__ __forceinline__ void store_frame(const LdsArgs& A, const FrameItem& it, const float2* buf) {
+  const int ch = A.ch, N = A.n_fft;
+  float* out = A.scratch + it.fg * (int64_t)N * ch;
+  for (int i = threadIdx.x; i < N; i += blockDim.x) {
     const float2 v = buf[i];
     const float w = A.win[i];
-    out[(int64_t)i * ch + c0] = v.x * w;
-    if (has1) out[(int64_t)i * ch + c1] = -v.y * w;
+    out[(int64_t)i * ch + it.c0] = v.x * w;
+    if (it.has1) out[(int64_t)i * ch + it.c1] = -v.y * w;
   }
 }
 
-// OLA gather of the any-size path: one thread per output position, all
-// channels; frames summed in ascending order (the reference's accumulation
-// order), sum w^2 likewise, normalise, output scale, chunk peak.
+template <int M, bool BLUE>
+__global__ __launch_bounds__(256) void k_stft_lds(LdsArgs A) {
+  __shared__ float2 buf[M];
+  const FrameItem it = frame_item(A, blockIdx.x, blockIdx.y);
+  load_frame(A, it, buf);
+  __syncthreads();
+  lds_dft<M, BLUE>(buf, A);
+  apply_gain(A, it, buf);
+  __syncthreads();
+  lds_dft<M, BLUE>(buf, A);
+  store_frame(A, it, buf);
+}
+
+// M > kLdsMaxM: blocks walk the (frame, pair) items; each owns two M-element
+// HBM buffers
+__global__ __launch_bounds__(1024) void k_stft_glb(LdsArgs A) {
+  const int npair = (A.ch + 1) / 2;
+  const int64_t items = A.total_frames * npair;
+  float2* w0 = A.work + (int64_t)blockIdx.x * 2 * A.M;
+  float2* w1 = w0 + A.M;
+  for (int64_t t = blockIdx.x; t < items; t += gridDim.x) {
+    const FrameItem it = frame_item(A, t / npair, (int)(t % npair));
+    load_frame(A, it, w0);
+    __syncthreads();
+    float2* r = glb_dft(w0, w1, A);
+    apply_gain(A, it, r);
+    __syncthreads();
+    r = glb_dft(r, r == w0 ? w1 : w0, A);
+    store_frame(A, it, r);
+    __syncthreads();
+  }
+}
+
+// OLA gather of the any-size path: one thread per output position and group of
+// up to 8 channels (grid.y); frames summed in ascending order (the reference's
+// accumulation order), sum w^2 likewise, normalise, output scale, chunk peak.
 __global__ __launch_bounds__(256) void k_ola_gather_lds(LdsArgs A) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= A.total_out) return;
@@ -803,6 +922,7 @@ __global__ __launch_bounds__(256) void k_ola_gather_lds(LdsArgs A) {
   const TomatisStream S = A.st[lo];
   const int64_t p = S.out_begin + (t - A.pos_base[lo]);
   const int hop = A.hop, N = A.n_fft, ch = A.ch;
+  const int cg = 8 * blockIdx.y, nc = min(8, ch - cg);
   const int64_t rel = p - S.first_start;
   int64_t jhi = floordiv(rel, hop);
   if (jhi > S.n_frames - 1) jhi = S.n_frames - 1;
@@ -812,18 +932,18 @@ __global__ __launch_bounds__(256) void k_ola_gather_lds(LdsArgs A) {
   float w = 0.f;
   for (int64_t j = jlo; j <= jhi; ++j) {
     const int off = (int)(rel - j * hop);
-    const float* src = A.scratch + ((S.frame_base + j) * (int64_t)N + off) * ch;
+    const float* src = A.scratch + ((S.frame_base + j) * (int64_t)N + off) * ch + cg;
 #pragma unroll
     for (int c = 0; c < 8; ++c)
-      if (c < ch) acc[c] = acc[c] + src[c];
+      if (c < nc) acc[c] = acc[c] + src[c];
     w = w + A.win2[off];
   }
   const float d = norm_den(w, A.norm_mode);
-  float* ys = A.y + S.out_off + (p - S.out_begin) * ch;
+  float* ys = A.y + S.out_off + (p - S.out_begin) * ch + cg;
   float mag = 0.f;
 #pragma unroll
   for (int c = 0; c < 8; ++c)
-    if (c < ch) {
+    if (c < nc) {
       const float o = (acc[c] / d) * S.out_scale;
       ys[c] = o;
       mag = fmaxf(mag, fabsf(o));
@@ -957,18 +1077,27 @@ void launch_gain_perm(int P, int NR, const float* gains, int n_rows, int n_bins,
 }
 
 void launch_lds_frames(const LdsArgs& A, hipStream_t s) {
+  if (A.M > kLdsMaxM) {
+    hipLaunchKernelGGL(k_stft_glb, dim3((unsigned)A.work_blocks), dim3(1024), 0, s, A);
+    return;
+  }
   const dim3 g((unsigned)A.total_frames, (unsigned)((A.ch + 1) / 2));
-#define LDS_N(NN) \
-  if (A.n_fft == NN) hipLaunchKernelGGL((k_stft_lds<NN>), g, dim3(256), 0, s, A);
+#define LDS_M(MM)                                                                      \
+  if (A.M == MM) {                                                                     \
+    if (A.blue) hipLaunchKernelGGL((k_stft_lds<MM, true>), g, dim3(256), 0, s, A);     \
+    else hipLaunchKernelGGL((k_stft_lds<MM, false>), g, dim3(256), 0, s, A);           \
+  }
 #ifndef TM_DEV_ONE_KERNEL
-  LDS_N(256) LDS_N(512) LDS_N(1024) LDS_N(2048) LDS_N(4096) LDS_N(8192)
+  LDS_M(2) LDS_M(4) LDS_M(8) LDS_M(16) LDS_M(32) LDS_M(64) LDS_M(128) LDS_M(256) LDS_M(512)
+  LDS_M(1024) LDS_M(2048) LDS_M(4096) LDS_M(8192) LDS_M(16384)
 #endif
-#undef LDS_N
+#undef LDS_M
 }
 
 void launch_lds_gather(const LdsArgs& A, hipStream_t s) {
   const int64_t ng = (A.total_out + 255) / 256;
-  hipLaunchKernelGGL(k_ola_gather_lds, dim3((unsigned)ng), dim3(256), 0, s, A);
+  hipLaunchKernelGGL(k_ola_gather_lds, dim3((unsigned)ng, (unsigned)((A.ch + 7) / 8)), dim3(256),
+                     0, s, A);
 }
 
 void launch_ola_gather(const MainArgs& A, int n_streams, const int64_t* pos_base, int64_t total,

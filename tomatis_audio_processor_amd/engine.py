@@ -315,16 +315,23 @@ def _alloc_out(torch, lens, ch, device):
     return torch.empty(max(1, tot), dtype=torch.float32, device=device), offs
 
 
+MAX_N_FFT = 1 << 16   # tm_shared.h kMaxNfft
+MAX_CHANNELS = 128    # tm_shared.h kMaxCh
+
+
 def _check_fft(n_fft, hop, ch):
     """Shapes the gfx950 library takes: register kernels for n_fft 2048 / 4096
-    with <= 2 channels, the any-size LDS path for every other power of two in
-    [256, 8192] and for 3..8 channels (tm_transform.hip)."""
-    if not (256 <= n_fft <= 8192) or (n_fft & (n_fft - 1)):
-        raise ValueError(f"n_fft={n_fft}: the gfx950 kernels take powers of two in [256, 8192]")
+    with <= 2 channels; the any-size path (tm_transform.hip: Stockham FFT,
+    Bluestein for n_fft that are not powers of two) for every other n_fft in
+    [2, 65536] and up to 128 channels.  The reference's np.fft.rfft/irfft take
+    any length (src/process_tomatis.py:396-398); hop outside [1, n_fft] is the
+    only shape it cannot run either (a zero hop never advances)."""
     if not (1 <= hop <= n_fft):
         raise ValueError(f"hop={hop} must be in [1, n_fft]")
-    if not (1 <= ch <= 8):
-        raise ValueError(f"{ch} channels: the gfx950 kernels handle 1 to 8 channels")
+    if not (2 <= n_fft <= MAX_N_FFT):
+        raise ValueError(f"n_fft={n_fft}: the gfx950 kernels take 2 <= n_fft <= {MAX_N_FFT}")
+    if not (1 <= ch <= MAX_CHANNELS):
+        raise ValueError(f"{ch} channels: the gfx950 kernels handle 1 to {MAX_CHANNELS} channels")
 
 
 # ---------------------------------------------------------------------------
