@@ -46,6 +46,16 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in DEPS)
 
 
+def _stale(obj: str, src: str) -> bool:
+    """A unit recompiles when its object is missing or older than its source,
+    a shared header or this script (objects are kept next to the library)."""
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    deps = [os.path.join(CSRC, src)] + [d for d in DEPS if not d.endswith(".hip")]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
 def build(force: bool = False, verbose: bool = True, out: str = OUT, extra=()) -> str:
     """Compile the C-ABI library; ``out``/``extra`` build experiment variants."""
     if out == OUT and not extra and not force and not needs_build():
@@ -53,21 +63,26 @@ def build(force: bool = False, verbose: bool = True, out: str = OUT, extra=()) -
     objs, procs = [], []
     for src, fl in UNITS.items():
         obj = f"{out}.{src}.o"
-        cmd = [HIPCC, *FLAGS, *fl, *extra, "-c", "-o", obj, os.path.join(CSRC, src)]
+        objs.append(obj)
+        if not force and not extra and not _stale(obj, src):
+            continue
+        cmd = [HIPCC, *FLAGS, *fl, *extra, "-c", "-o", obj + ".tmp", os.path.join(CSRC, src)]
         if verbose:
             print(" ".join(cmd), flush=True)
-        procs.append(subprocess.Popen(cmd))
-        objs.append(obj)
-    rcs = [p.wait() for p in procs]
+        procs.append((subprocess.Popen(cmd), obj))
+    rcs = [p.wait() for p, _ in procs]
     if any(rcs):
         raise subprocess.CalledProcessError(max(rcs), "hipcc")
+    for _, obj in procs:
+        os.replace(obj + ".tmp", obj)
     link = [HIPCC, ARCH, "-shared", "-fPIC", "-o", out + ".tmp", *objs]
     if verbose:
         print(" ".join(link), flush=True)
     subprocess.run(link, check=True)
     os.replace(out + ".tmp", out)
-    for o in objs:
-        os.remove(o)
+    if extra or out != OUT:
+        for o in objs:
+            os.remove(o)
     return out
 
 

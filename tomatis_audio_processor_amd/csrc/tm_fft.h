@@ -43,19 +43,46 @@ struct FftGeo {
 // operations of a wave execute in order, so the writes before the add are
 // visible to the partner's reads after its poll.  Bounded spin: a stuck
 // partner sets the error flag instead of hanging the GPU.
+// Straight-line for the register allocator (a compiled spin loop and the
+// lane-0 branch between the exchange rounds of a kernel at 256 VGPRs made it
+// spill): lane 0's add (EXEC narrowed inside the asm) and the poll loop are one
+// inline-asm block; returns false on a timeout, which the caller reports.
+__device__ __forceinline__ bool pair_wait(uint32_t* ctr) {
+  const uint32_t addr =
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)ctr;  // LDS offset
+  uint32_t c, d, t;
+  uint64_t ex;
+  int left = 1 << 22;
+  __asm__ volatile(
+      "  s_waitcnt lgkmcnt(0)\n"            // this wave's exchange writes have landed
+      "  s_mov_b64 %[ex], exec\n"
+      "  s_mov_b64 exec, 1\n"
+      "  ds_add_rtn_u32 %[c], %[a], %[one]\n"
+      "  s_waitcnt lgkmcnt(0)\n"
+      "  s_mov_b64 exec, %[ex]\n"
+      "  v_readfirstlane_b32 %[t], %[c]\n"
+      "  s_and_b32 %[t], %[t], -2\n"
+      "  s_add_u32 %[t], %[t], 2\n"         // target = (old & ~1) + 2
+      "1:\n"
+      "  ds_read_b32 %[c], %[a]\n"
+      "  s_waitcnt lgkmcnt(0)\n"
+      "  v_readfirstlane_b32 %[d], %[c]\n"
+      "  s_sub_u32 %[d], %[d], %[t]\n"
+      "  s_cmp_gt_i32 %[d], -1\n"          // (int)(counter - target) >= 0: done
+      "  s_cbranch_scc1 2f\n"
+      "  s_sub_u32 %[n], %[n], 1\n"
+      "  s_cmp_eq_u32 %[n], 0\n"
+      "  s_cbranch_scc1 2f\n"
+      "  s_sleep 1\n"
+      "  s_branch 1b\n"
+      "2:\n"
+      : [c] "=&v"(c), [d] "=&s"(d), [t] "=&s"(t), [ex] "=&s"(ex), [n] "+s"(left)
+      : [a] "v"(addr), [one] "v"(1u)
+      : "scc", "memory");
+  return left != 0;
+}
 __device__ __forceinline__ void pair_barrier(uint32_t* ctr, uint32_t* err) {
-  uint32_t o = 0;
-  if ((threadIdx.x & 63) == 0)
-    o = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-  o = __builtin_amdgcn_readfirstlane(o);
-  const uint32_t target = (o & ~1u) + 2u;
-  for (int spin = 0; spin < (1 << 22); ++spin) {
-    const uint32_t c = __builtin_amdgcn_readfirstlane(
-        __hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
-    if ((int32_t)(c - target) >= 0) return;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  if (err && (threadIdx.x & 63) == 0) atomicOr(err, TOMATIS_ERR_PAIR_BARRIER);
+  if (!pair_wait(ctr) && err && (threadIdx.x & 63) == 0) atomicOr(err, TOMATIS_ERR_PAIR_BARRIER);
 }
 
 // LDS synchronisation for an exchange: wave-local when P == 64, the pair
