@@ -82,69 +82,3 @@ def test_adaptive_quiet_f64_8192():
     res, ref = _run("adaptive", x, sr, n_fft=8192, hop=2048)
     np.testing.assert_array_equal(res.stream_states(0), ref["states"])
     assert float(res.extra["thresholds"].cpu().numpy()[0]) == ref["threshold"]
-
-
-@pytest.mark.parametrize("hop,ch,mode", [(1024, 2, "standard"), (2048, 2, "standard"),
-                                         (1024, 2, "xfade"), (2048, 1, "adaptive"),
-                                         (512, 2, "standard")])
-def test_half_frames_4096(hop, ch, mode, monkeypatch):
-    """n_fft 4096 as two P = 64 waves per frame (sample parities, one spectral
-    exchange; tm_transform.hip H) against the oracle and against the two-wave
-    P = 128 kernel (TOMATIS_HALF4096=0) on 4 streams with many limiter chunks.
-    Reference: src/process_tomatis.py:394-406 (4096/2048 is its default)."""
-    torch, E = _engine()
-    from oracle import tomatis_oracle as orc
-    from tomatis_audio_processor_amd.synth import synth_stream
-    sr = 48000
-    lens = [sr * 12 + 333, sr * 5, sr * 9 + 4096 + 7, sr * 3]
-    xs = [synth_stream(900 + i, n, ch, sr) for i, n in enumerate(lens)]
-    kw = dict(n_fft=4096, hop=hop)
-    outs = []
-    for half in ("1", "0"):
-        monkeypatch.setenv("TOMATIS_HALF4096", half)
-        ss = E.StreamSet.from_arrays(xs, sr)
-        if mode == "adaptive":
-            pipe = E.AdaptivePipeline(ss, **kw)
-        else:
-            pipe = E.GatePipeline(ss, gate_ui=50, **kw, **({"xfade_ms": 300.0} if mode == "xfade" else {}))
-        res = pipe.run()
-        torch.cuda.synchronize()
-        outs.append(res)
-    r1, r0 = outs
-    for i, (x, n) in enumerate(zip(xs, lens)):
-        y1, y0 = r1.output(i), r0.output(i)
-        # the two kernels differ only by float rounding of the transform
-        assert np.max(np.abs(y1 - y0)) <= 2e-5 * max(1.0, float(np.max(np.abs(y0))))
-        if i < 2:  # and against the oracle
-            if mode == "adaptive":
-                ref = orc.process_adaptive(x, sr, **kw)
-                mk = ref["wsum"] >= TAU
-                np.testing.assert_array_equal(r1.stream_states(i), ref["states"])
-            else:
-                ref = orc.process_standard(x, sr, gate_ui=50, **kw,
-                                           **({"xfade_ms": 300.0} if mode == "xfade" else {}))
-                mk = ref["wsum"][ref["pad"]:ref["pad"] + n] >= TAU
-                np.testing.assert_array_equal(r1.stream_states(i), ref["states"])
-            _check_chunks_stream(r1, i, ref, y1, mk, mode)
-
-
-def _check_chunks_stream(res, i, ref, y, m, mode):
-    """test_gpu_parity._check_chunks for stream i of a multi-stream result."""
-    from tomatis_audio_processor_amd import conditioning
-    from tests.test_gpu_parity import _scale_of, TOL
-    flags = res.scale_flags(i)
-    ranges = res.chunk_ranges(i)
-    peaks = res.stream_peaks(i)
-    yr = np.asarray(ref["y"], np.float64)
-    ref_scales = ref["scales"] if mode != "adaptive" else [ref["scale"] or 1.0]
-    assert len(ranges) == len(ref_scales)
-    for c, (a, b) in enumerate(ranges):
-        if b <= a:
-            continue
-        gs, rs = _scale_of(peaks[c]), float(ref_scales[c] or 1.0)
-        mm = m[a:b]
-        if abs(gs / rs - 1.0) > conditioning.ETA:
-            assert flags[c]
-        err = (np.abs(y[a:b][mm] - yr[a:b][mm]) if not flags[c]
-               else np.abs(y[a:b][mm] / gs - yr[a:b][mm] / rs) * min(gs, rs))
-        assert float(err.max(initial=0.0)) <= TOL, f"chunk {c}: {err.max()}"

@@ -1344,9 +1344,6 @@ struct tomatis_plan_s {
   int edge_mask = 0;      // set for one tomatis_stft_ola_limited_edges call
   int fuse_enabled = 1;   // TOMATIS_OPT_FUSE_LIMITER
   int lim_spin = 1 << 18; // TOMATIS_OPT_LIMITER_SPIN: fused-limiter wait bound (polls)
-  // n_fft 4096 as two P = 64 waves per frame (parities), TOMATIS_HALF4096
-  bool half = false;
-  cf* twX = nullptr;
   // run-scan gate (exclusive on/off predicates)
   bool gate_excl = false;
   void* gsum = nullptr;
@@ -1430,7 +1427,7 @@ int tomatis_plan_destroy(tomatis_plan_t p) {
                   p->grp_base, p->leaf_base, p->leaves, p->gsum, p->gcarry, p->gcarry_in,
                   p->aq, p->afin, p->acin,
                   p->chunk_need, p->chunk_done, p->chunk_rng, p->err, p->twL,
-                  p->pw_leaf, p->pw_prog, p->blue_b, p->blue_h, p->glb_work, p->twX};
+                  p->pw_leaf, p->pw_prog, p->blue_b, p->blue_h, p->glb_work};
   for (void* q : ptrs) dfree(q);
   delete p;
   return TOMATIS_OK;
@@ -1510,7 +1507,7 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
   // blocks, every wave busy to the end), at least 48 frames per interior run
   // so the rmax-1 warm-up frames per run stay a few percent.
   const int rmax_ = (N + hop - 1) / hop;
-  const bool fast_ok = !p->generic && (P == 64 || p->half) && env_int("TOMATIS_FAST_LOOP", 1) != 0;
+  const bool fast_ok = !p->generic && P == 64 && env_int("TOMATIS_FAST_LOOP", 1) != 0;
   std::vector<int64_t> e_lo(ns, 0), e_hi(ns, 0);
   int64_t fast_total = 0, n_edge = 0;
   for (int s = 0; s < ns; ++s) {
@@ -1715,39 +1712,24 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
     }
     p->rmax = (N + hop - 1) / hop;
     if (!p->lds) {  // register kernels only (NR = 16 or 32)
-      // half frames: the P = 64 tables of the 2048-point FFT each wave runs
-      const int Pt = p->half ? 64 : P, NRr = p->NR, Nt = Pt * NRr;
+      const int NRr = p->NR;
       // scaled-DIF output scales of the register FFT (tm_common.h): the step-2
       // table absorbs the forward NR-point DFT's, the synthesis window the
       // inverse's (whose inputs carry 1 / the forward's)
       const double* sigF = NRr == 32 ? splan<32, 0>().sig : splan<16, 0>().sig;
       const double* sigI = NRr == 32 ? splan<32, 2>().sig : splan<16, 2>().sig;
-      std::vector<cf> twN((size_t)NRr * Pt), twP(Pt);
+      std::vector<cf> twN((size_t)NRr * P), twP(P);
       for (int k2 = 0; k2 < NRr; ++k2)
-        for (int n1 = 0; n1 < Pt; ++n1) {
-          const double ang = -2.0 * M_PI * (double)((int64_t)n1 * k2 % Nt) / (double)Nt;
-          twN[((size_t)(k2 >> 1) * Pt + n1) * 2 + (k2 & 1)] = {(float)(cos(ang) * sigF[k2]),
-                                                              (float)(sin(ang) * sigF[k2])};
+        for (int n1 = 0; n1 < P; ++n1) {
+          const double ang = -2.0 * M_PI * (double)((int64_t)n1 * k2 % N) / (double)N;
+          twN[((size_t)(k2 >> 1) * P + n1) * 2 + (k2 & 1)] = {(float)(cos(ang) * sigF[k2]),
+                                                             (float)(sin(ang) * sigF[k2])};
         }
-      // synthesis window x the inverse's output scale of the register holding
-      // sample t (half frames: t = h + 2 (L + 64 i))
       std::vector<float> winS(N);
-      for (int t = 0; t < N; ++t)
-        winS[t] = (float)((double)w[t] * sigI[p->half ? (t >> 1) / Pt : t / Pt]);
-      for (int m = 0; m < Pt; ++m) {
-        const double ang = -2.0 * M_PI * (double)m / (double)Pt;
+      for (int t = 0; t < N; ++t) winS[t] = (float)((double)w[t] * sigI[t / P]);
+      for (int m = 0; m < P; ++m) {
+        const double ang = -2.0 * M_PI * (double)m / (double)P;
         twP[m] = {(float)cos(ang), (float)sin(ang)};
-      }
-      if (p->half) {  // W_4096^bin of (lane L, register i) of the 2048-point layout
-        std::vector<cf> twX((size_t)Nt);
-        for (int i = 0; i < NRr; ++i)
-          for (int L = 0; L < Pt; ++L) {
-            const int jp = i >> 3, dd = i & 7;
-            const int kb = ((L / 8) + 8 * jp) + NRr * ((L % 8) + 8 * dd);  // tm_fft.h fft_bin
-            const double ang = -2.0 * M_PI * (double)kb / (double)N;
-            twX[((size_t)(i >> 1) * Pt + L) * 2 + (i & 1)] = {(float)cos(ang), (float)sin(ang)};
-          }
-        if ((rc = dalloc_copy(&p->twX, twX))) return rc;
       }
       if ((rc = dalloc_copy(&p->winS, winS))) return rc;
       if ((rc = dalloc_copy(&p->twN, twN))) return rc;
@@ -1932,7 +1914,6 @@ int tomatis_plan_create(tomatis_plan_t* out, const TomatisPlanDesc* desc, const 
   }
   p->P = p->lds ? 64 : ((N == 2048 && env_int("TOMATIS_P64", 1)) ? 64 : 128);
   p->NR = N / p->P;
-  p->half = !p->lds && N == 4096 && p->P == 128 && env_int("TOMATIS_HALF4096", 0) != 0;
   p->SH = (!p->lds && hop % p->P == 0) ? hop / p->P : 0;
   p->generic = p->lds || (p->NR == 16 ? !(p->SH == 2 || p->SH == 4 || p->SH == 8)
                                       : !(p->SH == 4 || p->SH == 8 || p->SH == 16));
@@ -2273,7 +2254,7 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
       return TOMATIS_E_NOMEM;
     p->gperm_rows = n_rows;
   }
-  launch_gain_perm(p->half ? 64 : p->P, p->NR, gains, n_rows, N / 2 + 1, p->gperm, s, p->half ? 1 : 0);
+  launch_gain_perm(p->P, p->NR, gains, n_rows, N / 2 + 1, p->gperm, s);
   MainArgs A;
   A.x = x;
   A.y = y;
@@ -2287,8 +2268,6 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
   A.win2 = p->win2;
   A.twN = p->twN;
   A.twP = p->twP;
-  A.twX = p->twX;
-  A.half = p->half ? 1 : 0;
   A.winv = p->winv;
   A.scratch = p->scratch;
   A.n_runs = p->n_runs;
@@ -2298,13 +2277,12 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
   A.norm_mode = p->d.norm_mode;
   A.rmax = p->generic ? 1 : p->rmax;
   A.inv_n = 1.0f / (float)N;
-  A.n_rows_lds = (n_rows <= 2 && (N <= 2048 || p->half)) ? n_rows : 0;
+  A.n_rows_lds = (n_rows <= 2 && N <= 2048) ? n_rows : 0;
   A.lds_mixed = 0;
   A.edge_mask = p->edge_mask;
   A.lds_row[0] = 0;
   A.lds_row[1] = 1;
-  if (n_rows > 2 && (N <= 2048 || p->half) && p->d.alpha_mode != 0 &&
-      env_int("TOMATIS_GAIN_LDS", 1) != 0) {
+  if (n_rows > 2 && N <= 2048 && p->d.alpha_mode != 0 && env_int("TOMATIS_GAIN_LDS", 1) != 0) {
     // cross-fade tables: the pure rows (alpha 0 and 1) carry most frames
     // (xfade: rows 0/1; adaptive: rows 2 and 2 + xfade_frames = n_rows - 1)
     A.n_rows_lds = 2;
@@ -2320,6 +2298,7 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
   A.chunk_rng = p->chunk_rng;
   A.err = p->err;
   A.lim_spin = p->lim_spin;
+  A.lim_rev = env_int("TOMATIS_LIM_REV", 0);
   A.prof = nullptr;
   if (limit > 0.f) {
     if (!p->chunk_done) return TOMATIS_E_UNSUPPORTED;

@@ -41,8 +41,6 @@ struct MainArgs {
   const float* win2;    // [N] win*win (f32)
   const cf* twN;        // [32][P]
   const cf* twP;        // [P]
-  const cf* twX;        // half frames (n_fft 4096 as 2 x 2048): W_4096^bin per lane/register
-  int half;             // 1: half-frame kernel (two P = 64 waves per 4096-sample frame)
   const float* winv;    // [hop] 1/(interior wsum) (already normalisation-rule applied)
   cf* scratch;          // generic path: [frames][N]
   int n_runs, hop, n_bins, ch, norm_mode, rmax, n_rows_lds;
@@ -58,6 +56,7 @@ struct MainArgs {
   const int64_t* chunk_rng;  // [2 * chunk]: output-relative [p0, p1)
   uint32_t* err;        // TOMATIS_ERR_* bits
   int lim_spin;         // fused-limiter wait bound (polls of the chunk counter)
+  int lim_rev;          // rescale newest output first (TOMATIS_LIM_REV)
   unsigned long long* prof;  // TM_PROFILE builds only: per-phase wave cycles
 };
 
@@ -98,7 +97,7 @@ int transform_slots_per_cu(int P, int NR);  // resident sequences per CU
 void launch_transform(const MainArgs& A, int P, int NR, int SH, int ch, int wg, hipStream_t s);
 void launch_frames(const MainArgs& A, int P, int NR, int blocks, hipStream_t s);
 void launch_gain_perm(int P, int NR, const float* gains, int n_rows, int n_bins, float* out,
-                      hipStream_t s, int half = 0);
+                      hipStream_t s);
 void launch_ola_gather(const MainArgs& A, int n_streams, const int64_t* pos_base, int64_t total,
                        int N, hipStream_t s);
 int env_int(const char* name, int dflt);

@@ -116,7 +116,10 @@ __device__ void limit_own(const MainArgs& A, const TomatisStream& S, int gc, int
   f4v* b4 = reinterpret_cast<f4v*>(base);
   const int64_t n4 = n >> 2;
   constexpr int U = 16;
-  for (int64_t i = lane; i < n4; i += 64 * U) {
+  // blocks of 64 U float4 (A.lim_rev: newest first, while the MALL still holds it)
+  const int64_t nb = (n4 + 64 * U - 1) / (64 * U);
+  for (int64_t j = 0; j < nb; ++j) {
+    const int64_t i = (A.lim_rev ? nb - 1 - j : j) * (64 * U) + lane;
     f4v t[U];
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -190,51 +193,27 @@ typedef __attribute__((address_space(4))) const uint32_t cu32;
 // GM: where the gain rows live (per-lane layout).  0: global (L2) only;
 // 1: all (<= 2) rows in LDS; 2: the two pure rows A.lds_row[0..1] in LDS, the
 // cross-fade lattice rows from global (row is wave-uniform, so is the branch).
-//
-// H (half frames, n_fft 4096 = 2 x 2048): a sequence is two waves; wave h holds
-// the samples of parity h (lane L register i: frame sample h + 2 (L + 64 i)) and
-// runs the P = 64 register FFT on them (E = FFT_2048(even), O = FFT_2048(odd)).
-// X[k] = E + W^k O, X[k + 2048] = E - W^k O (W = W_4096), so with the 4096-bin
-// gain G the inverse's even / odd halves are
-//   Ye = A E + B (W^k O),  Yo = B (W^-k E) + A O,  A = G[k] + G[k+2048], B = G[k] - G[k+2048]
-// (both waves compute v = A v + B r from the partner's twiddled spectrum r),
-// then each wave runs the P = 64 inverse and the register OLA on its parity.
-// One spectral exchange per frame (8 rounds of 4 registers through the
-// sequence's LDS, pair barriers) instead of four two-wave exchanges.
-template <int P, int NR, int SH, int CH, int GM, bool PF, bool NT, int WG, bool H = false>
+template <int P, int NR, int SH, int CH, int GM, bool PF, bool NT, int WG>
 __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(MainArgs A) {
 #ifdef TM_PROFILE
   const unsigned long long t_k0 = __builtin_amdgcn_s_memtime();
   const unsigned long long rt_k0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  static_assert(!H || P == 64, "half frames run the P = 64 FFT per wave");
   using G = FftGeo<P, NR>;
-  constexpr int N = G::N;              // FFT length (per wave when H)
-  constexpr int NPAR = H ? 2 : 1;      // sample parities (tables per parity)
-  constexpr int PS = NPAR * P;         // lanes per sequence
-  constexpr int NF = NPAR * N;         // frame length
-  constexpr int NSEQ = WG / PS;
-  constexpr int NBUF = H ? WG / 64 : NSEQ;  // round buffers (H: one per wave)
-  constexpr int HOP = SH * PS;
+  constexpr int N = G::N;
+  constexpr int NSEQ = WG / P;
+  constexpr int HOP = SH * P;
   constexpr int NC = NR - SH;  // carried accumulator registers
   constexpr int SHQ = (SH + 3) & ~3;  // winv registers padded to a quad
   constexpr bool LT = P == 64;  // per-lane step-3 twiddle table
-  // gain rows in LDS: GM 1 / 2 hold two rows (H: each an A and a B half)
-  constexpr int GROW = NPAR * N;
   __shared__ __attribute__((aligned(16))) cf s_twN[NR * P];
   __shared__ __attribute__((aligned(16))) cf s_twP[LT ? 8 * P : P];
-  __shared__ __attribute__((aligned(16))) float s_win[NPAR][N];      // lane-quad layout
-  __shared__ __attribute__((aligned(16))) float s_winS[NPAR][N];     // synthesis, scaled
-  __shared__ __attribute__((aligned(16))) float s_winv[NPAR][SHQ * P];  // lane-quad layout
-  __shared__ cf s_buf[NBUF][G::SEQ_LDS];
-  __shared__ __attribute__((aligned(16))) float s_gain[GM ? 2 * GROW : 4];
-  __shared__ __attribute__((aligned(16))) cf s_twX[H ? N : 2];  // H: W_4096^bin, lane-pair layout
-  __shared__ uint32_t s_pair[H ? NSEQ : 1];                      // H: pair-barrier counters
+  __shared__ __attribute__((aligned(16))) float s_win[N];      // lane-quad layout
+  __shared__ __attribute__((aligned(16))) float s_winS[N];     // synthesis, scaled
+  __shared__ __attribute__((aligned(16))) float s_winv[SHQ * P];  // lane-quad layout
+  __shared__ cf s_buf[NSEQ][G::SEQ_LDS];
+  __shared__ __attribute__((aligned(16))) float s_gain[GM ? 2 * N : 4];
   for (int i = threadIdx.x; i < NR * P; i += WG) s_twN[i] = A.twN[i];
-  if constexpr (H) {
-    for (int i = threadIdx.x; i < N; i += WG) s_twX[i] = A.twX[i];
-    if (threadIdx.x < NSEQ) s_pair[threadIdx.x] = 0u;
-  }
   if constexpr (LT) {  // [m/2][l][m&1] = W_P^{(l%8)*m}
     for (int i = threadIdx.x; i < 8 * P; i += WG) {
       const int m = 2 * (i / (2 * P)) + (i & 1), l = (i / 2) % P;
@@ -243,45 +222,35 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   } else {
     for (int i = threadIdx.x; i < P; i += WG) s_twP[i] = A.twP[i];
   }
-  // frame sample of (parity h, lane l, register i)
-  auto fpos = [](int h, int l, int i) { return H ? h + 2 * (l + P * i) : l + P * i; };
-  for (int e = threadIdx.x; e < NPAR * N; e += WG) {  // e = lq(i, l) per parity
-    const int h = e / N, ee = e % N;
-    const int q = ee >> 2, l = q % P, i = (q / P) * 4 + (ee & 3);
-    s_win[h][ee] = A.win[fpos(h, l, i)];
-    s_winS[h][ee] = A.winS[fpos(h, l, i)];
+  for (int e = threadIdx.x; e < N; e += WG) {  // e = lq(i, l)
+    const int q = e >> 2, l = q % P, i = (q / P) * 4 + (e & 3);
+    s_win[e] = A.win[l + P * i];
+    s_winS[e] = A.winS[l + P * i];
   }
-  for (int e = threadIdx.x; e < NPAR * SHQ * P; e += WG) {
-    const int h = e / (SHQ * P), ee = e % (SHQ * P);
-    const int q = ee >> 2, l = q % P, i = (q / P) * 4 + (ee & 3);
-    s_winv[h][ee] = (i < SH) ? A.winv[fpos(h, l, i)] : 0.f;
+  for (int e = threadIdx.x; e < SHQ * P; e += WG) {
+    const int q = e >> 2, l = q % P, i = (q / P) * 4 + (e & 3);
+    s_winv[e] = (i < SH) ? A.winv[l + P * i] : 0.f;
   }
   if constexpr (GM == 1) {
     const int nr = A.n_rows_lds;
-    for (int i = threadIdx.x; i < nr * GROW; i += WG) s_gain[i] = A.gains[i];
+    for (int i = threadIdx.x; i < nr * N; i += WG) s_gain[i] = A.gains[i];
   } else if constexpr (GM == 2) {
-    for (int i = threadIdx.x; i < 2 * GROW; i += WG)
-      s_gain[i] = A.gains[(int64_t)A.lds_row[i >= GROW] * GROW + (i >= GROW ? i - GROW : i)];
+    for (int i = threadIdx.x; i < 2 * N; i += WG)
+      s_gain[i] = A.gains[(int64_t)A.lds_row[i >= N] * N + (i >= N ? i - N : i)];
   }
   if constexpr (P > 64) {  // pair-barrier counters (tm_fft.h)
     if (threadIdx.x < NSEQ) reinterpret_cast<uint32_t*>(s_buf[threadIdx.x] + G::BUF)[0] = 0u;
   }
   __syncthreads();
-  // wave parity (H) and the per-parity tables
-  const int hw = H ? (int)__builtin_amdgcn_readfirstlane((threadIdx.x >> 6) & 1) : 0;
-  const float4* const w4 = reinterpret_cast<const float4*>(s_win[hw]);
-  const float4* const ws4 = reinterpret_cast<const float4*>(s_winS[hw]);
-  const float4* const wv4 = reinterpret_cast<const float4*>(s_winv[hw]);
+  const float4* const w4 = reinterpret_cast<const float4*>(s_win);
+  const float4* const ws4 = reinterpret_cast<const float4*>(s_winS);
 #ifdef TM_PROFILE
   const unsigned long long t_k1 = __builtin_amdgcn_s_memtime();
 #endif
 
-  const int seq0 = threadIdx.x / PS, L0 = threadIdx.x % P;
-  // lane L register i holds frame sample Lx + PX * i
-  constexpr int PX = PS;
+  const int seq = threadIdx.x / P, L = threadIdx.x % P;
   // wave-uniform run id (readfirstlane: run and stream descriptors load as scalars)
-  const int run_id = __builtin_amdgcn_readfirstlane(blockIdx.x * NSEQ + seq0);
-  const int L = L0, seq = seq0, Lx = H ? hw + 2 * L0 : L0;
+  const int run_id = __builtin_amdgcn_readfirstlane(blockIdx.x * NSEQ + seq);
   Run R{0, 0, 0, 0};
   const bool valid = run_id < A.n_runs;
   if (valid) R = A.runs[run_id];
@@ -291,7 +260,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   const TomatisStream S = A.st[R.s];
   const int64_t kfirst = max<int64_t>(0, R.ka - (A.rmax - 1));
   const int nit = valid ? (int)(R.kb - kfirst) : 0;
-  cf* buf = s_buf[H ? (int)(threadIdx.x >> 6) : seq];
+  cf* buf = s_buf[seq];
   const float* xs = A.x + S.in_off;
   float* ys = A.y + S.out_off;
   const int64_t out_end = S.out_begin + S.out_len;
@@ -299,7 +268,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   const float iscale = S.in_scale;
 
   if (valid && R.ka == 0 && S.first_start > S.out_begin) {  // adaptive: zeros before frame 0
-    for (int64_t p = S.out_begin + Lx; p < min(S.first_start, out_end); p += PX)
+    for (int64_t p = S.out_begin + L; p < min(S.first_start, out_end); p += P)
       store_cf<CH>(ys, p - S.out_begin, cf{0.f, 0.f});
   }
 
@@ -317,65 +286,11 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   cf acc[NC];
 #pragma unroll
   for (int i = 0; i < NC; ++i) acc[i] = {0.f, 0.f};
-  bool pair_ok = true;  // H: every exchange barrier completed (reported after the run)
 
 #ifdef TM_PROFILE
   unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long tlast = __builtin_amdgcn_s_memtime();
 #endif
-  // H: spectral exchange with the partner wave and the two-coefficient gain
-  // (header comment).  Rounds of 4 registers through two 256-entry halves of
-  // the wave's round buffer, alternating, one pair barrier per round: a half
-  // is rewritten two rounds later, after the partner has passed the barrier
-  // that follows its reads.  Rows: [A half | B half] per row, per-lane layout.
-  auto exchange_gain = [&](cf (&v)[NR], uint32_t row) {
-    if constexpr (H) {
-      uint32_t* const ctr = &s_pair[seq];
-      const float sgn = (float)(2 * hw - 1);  // wave 0 sends W^-k E, wave 1 W^k O (no branch)
-      cf* const mine = s_buf[threadIdx.x >> 6];
-      const cf* const theirs = s_buf[(threadIdx.x >> 6) ^ 1];
-      bool g_lds = GM == 1;
-      if constexpr (GM == 2) g_lds = row == A.lds_row[0] || row == A.lds_row[1];
-      const float* const gl =
-          s_gain + ((GM == 1 ? row : row == A.lds_row[1]) ? GROW : 0);
-      const __amdgpu_buffer_rsrc_t rg = mk_rsrc(A.gains + (int64_t)row * GROW, GROW * 4);
-#pragma unroll
-      for (int q = 0; q < NR / 4; ++q) {
-        const int half = (q & 1) * 256;
-        // send this wave's 4 registers, twiddled: wave 0 W^-k E, wave 1 W^k O
-#pragma unroll
-        for (int u2 = 0; u2 < 2; ++u2) {
-          const float4 t = reinterpret_cast<const float4*>(s_twX)[(2 * q + u2) * P + L];
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            const int i = 4 * q + 2 * u2 + u;
-            const cf w = u ? cf{t.z, t.w * sgn} : cf{t.x, t.y * sgn};
-            mine[half + (2 * u2 + u) * P + L] = cmul(v[i], w);
-          }
-        }
-        pair_ok &= pair_wait(ctr);
-        float4 ga, gb;
-        if (g_lds) {
-          ga = reinterpret_cast<const float4*>(gl)[q * P + L];
-          gb = reinterpret_cast<const float4*>(gl + N)[q * P + L];
-        } else {
-          const f32x4 a4 = __builtin_amdgcn_raw_buffer_load_b128(rg, L * 16, q * P * 16, 0);
-          const f32x4 b4 = __builtin_amdgcn_raw_buffer_load_b128(rg, L * 16, (N + q * P * 4) * 4, 0);
-          ga = make_float4(__uint_as_float(a4.x), __uint_as_float(a4.y), __uint_as_float(a4.z),
-                           __uint_as_float(a4.w));
-          gb = make_float4(__uint_as_float(b4.x), __uint_as_float(b4.y), __uint_as_float(b4.z),
-                           __uint_as_float(b4.w));
-        }
-        const float aa[4] = {ga.x, ga.y, ga.z, ga.w}, bb[4] = {gb.x, gb.y, gb.z, gb.w};
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int i = 4 * q + u;
-          const cf r = theirs[half + u * P + L];
-          v[i] = {__builtin_fmaf(aa[u], v[i].x, bb[u] * r.x), __builtin_fmaf(aa[u], v[i].y, bb[u] * r.y)};
-        }
-      }
-    }
-  };
   // window -> FFT -> gain row -> IFFT -> window, OLA into the accumulator
   auto transform = [&](cf (&v)[NR], uint32_t row) {
       // ---- analysis window (x * in_scale first, two roundings as the reference) ----
@@ -394,9 +309,6 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       TPROF(1, v[NR - 1].x);
       fft_fwd<P, NR, LT>(v, L, s_twN, s_twP, buf, A.err);
       TPROF(2, v[NR - 1].x);
-      if constexpr (H) {
-        exchange_gain(v, row);
-      } else {
       // ---- gain row (real, even, 1/N folded in), per-lane layout ----
       bool g_lds = GM == 1;
       if constexpr (GM == 2) g_lds = row == A.lds_row[0] || row == A.lds_row[1];
@@ -422,7 +334,6 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
           v[4 * n4 + 3] = cscale(v[4 * n4 + 3], __uint_as_float(g.w));
         }
       }
-      }
       TPROF(3, v[NR - 1].x);
       fft_inv<P, NR, LT>(v, L, s_twN, s_twP, buf, A.err);
       TPROF(4, v[NR - 1].x);
@@ -447,7 +358,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
     float wv[SHQ];
 #pragma unroll
     for (int q = 0; q < SHQ / 4; ++q) {
-      const float4 t = wv4[q * P + L];
+      const float4 t = reinterpret_cast<const float4*>(s_winv)[q * P + L];
       wv[4 * q] = t.x;
       wv[4 * q + 1] = t.y;
       wv[4 * q + 2] = t.z;
@@ -456,8 +367,8 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
 #pragma unroll
     for (int i = 0; i < SH; ++i) {
       const cf o = cscale(cscale(v[i], wv[i]), oscale);
-      if constexpr (NT) bstore<CH, 2>(o, ry, Lx * CH * 4, so + PX * i * CH * 4);
-      else bstore<CH>(o, ry, Lx * CH * 4, so + PX * i * CH * 4);
+      if constexpr (NT) bstore<CH, 2>(o, ry, L * CH * 4, so + P * i * CH * 4);
+      else bstore<CH>(o, ry, L * CH * 4, so + P * i * CH * 4);
       pk = fmaxf(pk, cmag<CH>(o));
     }
   };
@@ -472,7 +383,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
     const int nwarm = (int)(R.ka - kfirst);
     const int64_t s0 = S.first_start + kfirst * HOP;
     const __amdgpu_buffer_rsrc_t rx =
-        mk_rsrc(xs + CH * s0, (uint32_t)(((int64_t)(nit - 1) * HOP + NF) * CH * 4));
+        mk_rsrc(xs + CH * s0, (uint32_t)(((int64_t)(nit - 1) * HOP + N) * CH * 4));
     const __amdgpu_buffer_rsrc_t ry =
         mk_rsrc(ys + CH * (s_ka - S.out_begin), (uint32_t)((int64_t)(nit - nwarm) * HOP * CH * 4));
     // gain-row ids through the scalar cache: the aligned 32-bit word holding the
@@ -497,22 +408,22 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       const int so = it * (HOP * CH * 4);
 #pragma unroll
       for (int n2 = 0; n2 < NO; ++n2) {  // the frame's first hop is read for the last time (nt)
-        if (NT && n2 < SH) dst[n2] = bload<CH, 2>(rx, Lx * CH * 4, so + PX * n2 * CH * 4);
-        else dst[n2] = bload<CH>(rx, Lx * CH * 4, so + PX * n2 * CH * 4);
+        if (NT && n2 < SH) dst[n2] = bload<CH, 2>(rx, L * CH * 4, so + P * n2 * CH * 4);
+        else dst[n2] = bload<CH>(rx, L * CH * 4, so + P * n2 * CH * 4);
       }
     };
     auto ld_new = [&](int it, cf (&dst)[SH]) {
-      const int so = it * (HOP * CH * 4) + PX * NO * CH * 4;
+      const int so = it * (HOP * CH * 4) + P * NO * CH * 4;
 #pragma unroll
-      for (int j = 0; j < SH; ++j) dst[j] = bload<CH>(rx, Lx * CH * 4, so + PX * j * CH * 4);
+      for (int j = 0; j < SH; ++j) dst[j] = bload<CH>(rx, L * CH * 4, so + P * j * CH * 4);
     };
     const __amdgpu_buffer_rsrc_t rnull = mk_rsrc(ys, 0u);
     float wv[SHQ];
     auto store_out = [&](const cf (&o)[SH], __amdgpu_buffer_rsrc_t r, int so) {
 #pragma unroll
       for (int i = 0; i < SH; ++i) {
-        if constexpr (NT) bstore<CH, 2>(o[i], r, Lx * CH * 4, so + PX * i * CH * 4);
-        else bstore<CH>(o[i], r, Lx * CH * 4, so + PX * i * CH * 4);
+        if constexpr (NT) bstore<CH, 2>(o[i], r, L * CH * 4, so + P * i * CH * 4);
+        else bstore<CH>(o[i], r, L * CH * 4, so + P * i * CH * 4);
       }
     };
     cf v[NR], nh[SH], o[SH];
@@ -545,7 +456,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       // outputs of this frame's first hop: interior 1/sum w^2, output scale, peak
 #pragma unroll
       for (int q = 0; q < SHQ / 4; ++q) {
-        const float4 t4 = wv4[q * P + L];
+        const float4 t4 = reinterpret_cast<const float4*>(s_winv)[q * P + L];
         wv[4 * q] = t4.x;
         wv[4 * q + 1] = t4.y;
         wv[4 * q + 2] = t4.z;
@@ -584,19 +495,19 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
     auto load_frame = [&](int64_t kk, cf (&dst)[NR]) {
       const bool lv = valid && (kk < R.kb);
       const int64_t sk = S.first_start + kk * HOP;
-      if (lv && sk >= 0 && sk + NF <= S.n) {
-        const __amdgpu_buffer_rsrc_t rx = mk_rsrc(xs + CH * sk, NF * CH * 4);
+      if (lv && sk >= 0 && sk + N <= S.n) {
+        const __amdgpu_buffer_rsrc_t rx = mk_rsrc(xs + CH * sk, N * CH * 4);
   #pragma unroll
         for (int n2 = 0; n2 < NR; ++n2) {
           // the frame's first hop is read for the last time: stream it (nt)
-          if (NT && n2 < SH) dst[n2] = bload<CH, 2>(rx, Lx * CH * 4, PX * n2 * CH * 4);
-          else dst[n2] = bload<CH>(rx, Lx * CH * 4, PX * n2 * CH * 4);
+          if (NT && n2 < SH) dst[n2] = bload<CH, 2>(rx, L * CH * 4, P * n2 * CH * 4);
+          else dst[n2] = bload<CH>(rx, L * CH * 4, P * n2 * CH * 4);
         }
       } else {
-        const int Lo = opaque(Lx);
+        const int Lo = opaque(L);
   #pragma unroll
         for (int n2 = 0; n2 < NR; ++n2) {
-          const int64_t p = sk + Lo + PX * n2;
+          const int64_t p = sk + Lo + P * n2;
           dst[n2] = (lv && p >= 0 && p < S.n) ? load_cf<CH>(xs, p) : cf{0.f, 0.f};
         }
       }
@@ -638,12 +549,12 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
         if (full && !edge) {
           emit_full(v, mk_rsrc(ys + CH * (s_k - S.out_begin), HOP * CH * 4), 0);
         } else {
-          const int Lo = opaque(Lx);
+          const int Lo = opaque(L);
   #pragma unroll
           for (int i = 0; i < SH; ++i) {
-            const int64_t p = s_k + Lo + PX * i;
+            const int64_t p = s_k + Lo + P * i;
             if (p >= S.out_begin && p < out_end) {
-              const float d = norm_den(wsum_rel(p - S.first_start, S.n_frames, HOP, NF, A.win2),
+              const float d = norm_den(wsum_rel(p - S.first_start, S.n_frames, HOP, N, A.win2),
                                        A.norm_mode);
               const cf o = cscale(cf{v[i].x / d, v[i].y / d}, oscale);
               store_cf<CH>(ys, p - S.out_begin, o);
@@ -652,12 +563,12 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
           }
         }
         if ((R.last & 1) && k == R.kb - 1) {  // stream tail after the last frame
-          const int Lo = opaque(Lx);
+          const int Lo = opaque(L);
   #pragma unroll
           for (int i = SH; i < NR; ++i) {
-            const int64_t p = s_k + Lo + PX * i;
+            const int64_t p = s_k + Lo + P * i;
             if (p >= S.out_begin && p < out_end) {
-              const float d = norm_den(wsum_rel(p - S.first_start, S.n_frames, HOP, NF, A.win2),
+              const float d = norm_den(wsum_rel(p - S.first_start, S.n_frames, HOP, N, A.win2),
                                        A.norm_mode);
               const cf o = cscale(cf{v[i].x / d, v[i].y / d}, oscale);
               store_cf<CH>(ys, p - S.out_begin, o);
@@ -670,20 +581,18 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       for (int i = 0; i < NC; ++i) acc[i] = v[i + SH];
     }
   }
-  if constexpr (H) {
-    if (!pair_ok && L == 0) atomicOr(A.err, TOMATIS_ERR_PAIR_BARRIER);
-  }
   if (valid) flush_peak<P>(pk, cid, S, A.peaks, L, done);
   if (valid && done) {
     // this wave's own output range (stores of frames [ka, kb) and the stream tail)
     const int64_t s_last = S.first_start + (R.kb - 1) * HOP;
     const int64_t lo = max(s_ka, S.out_begin) - S.out_begin;
-    const int64_t hi = min(s_last + ((R.last & 1) ? (int64_t)NF : (int64_t)HOP), out_end) - S.out_begin;
+    const int64_t hi = min(s_last + ((R.last & 1) ? (int64_t)N : (int64_t)HOP), out_end) - S.out_begin;
     // P > 64: both waves of the sequence cover the same range; split it by wave
-    const int nw = PS / 64, w = H ? hw : (L >> 6);
+    const int nw = P / 64, w = L >> 6;
     const int64_t span = hi - lo, per = (span + nw - 1) / nw;
     const int64_t wlo = lo + per * w, whi = min(hi, wlo + per);
-    for (int c = cid_first; c <= cid; ++c) {
+    for (int cc = cid_first; cc <= cid; ++cc) {
+      const int c = A.lim_rev ? cid + cid_first - cc : cc;
       // edge chunks (shared with a neighbouring time shard) are scaled after
       // the peak exchange instead (tomatis_apply_limiter_edges)
       if (((A.edge_mask & 1) && c == 0) || ((A.edge_mask & 2) && c == S.n_chunks - 1)) continue;
@@ -780,22 +689,6 @@ __global__ void k_gain_perm(const float* __restrict__ g, int n_rows, int n_bins,
   b = (b <= N / 2) ? b : N - b;
   // x the forward FFT's output scale of register i (its step-3c DFT_8 output)
   out[t] = (g[(int64_t)row * n_bins + b] * (1.0f / (float)N)) * sig_at<8>(i & 7);
-}
-
-// half frames: rows [rows][n_bins = 2049] of the 4096-point gain -> [rows][A | B]
-// in the P = 64 per-lane layout, A = G[k] + G[k + 2048], B = G[k] - G[k + 2048]
-// (G[k + 2048] = g[2048 - k]), scaled by 1/4096 and the forward output scale
-__global__ void k_gain_perm_h(const float* __restrict__ g, int n_rows, int n_bins,
-                              float* __restrict__ out) {
-  constexpr int P = 64, NR = 32, N = P * NR;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n_rows * 2 * N) return;
-  const int row = t / (2 * N), r = t - row * 2 * N, part = r / N, e = r - part * N;
-  const int q = e >> 2, L = q % P, i = (q / P) * 4 + (e & 3);
-  const int k = fft_bin<P, NR>(L, i);
-  const float* gr = g + (int64_t)row * n_bins;
-  const float a = gr[k], b = gr[N - k];
-  out[t] = ((part ? a - b : a + b) * (1.0f / (float)(2 * N))) * sig_at<8>(i & 7);
 }
 
 // generic-hop OLA gather: one thread per output position (frame order preserved)
@@ -1070,27 +963,24 @@ void launch_main_pf(const MainArgs& A, int ch, hipStream_t s) {
   constexpr bool kNoLdsGains = P == 128 && NR == 32;
   const int gm = kNoLdsGains ? 0 : (A.n_rows_lds > 0 ? (A.lds_mixed ? 2 : 1) : 0);
   const dim3 g((A.n_runs + WG / P - 1) / (WG / P)), b(WG);
-#define TM_LAUNCH(CHv, GMv) \
-  hipLaunchKernelGGL((k_stft_ola<P, NR, SH, CHv, GMv, PF, NT, WG>), g, b, 0, s, A)
 #ifdef TM_DEV_ONE_KERNEL  // dev/asm studies: one instantiation (stereo, LDS gains)
   (void)gm;
   (void)ch;
-  TM_LAUNCH(2, 1);
+  hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 1, PF, NT, WG>), g, b, 0, s, A);
 #else
   if constexpr (kNoLdsGains) {
-    if (ch == 2) TM_LAUNCH(2, 0);
-    else TM_LAUNCH(1, 0);
+    if (ch == 2) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 0, PF, NT, WG>), g, b, 0, s, A);
+    else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, 0, PF, NT, WG>), g, b, 0, s, A);
   } else if (ch == 2) {
-    if (gm == 1) TM_LAUNCH(2, 1);
-    else if (gm == 2) TM_LAUNCH(2, 2);
-    else TM_LAUNCH(2, 0);
+    if (gm == 1) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 1, PF, NT, WG>), g, b, 0, s, A);
+    else if (gm == 2) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 2, PF, NT, WG>), g, b, 0, s, A);
+    else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 0, PF, NT, WG>), g, b, 0, s, A);
   } else {
-    if (gm == 1) TM_LAUNCH(1, 1);
-    else if (gm == 2) TM_LAUNCH(1, 2);
-    else TM_LAUNCH(1, 0);
+    if (gm == 1) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, 1, PF, NT, WG>), g, b, 0, s, A);
+    else if (gm == 2) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, 2, PF, NT, WG>), g, b, 0, s, A);
+    else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, 0, PF, NT, WG>), g, b, 0, s, A);
   }
 #endif
-#undef TM_LAUNCH
 }
 template <int P, int NR, int SH>
 void launch_main(const MainArgs& A, int ch, int wg, hipStream_t s) {
@@ -1148,45 +1038,10 @@ int transform_slots_per_cu(int P, int NR) {
   return (wg == 256 ? 2 : 1) * (wg / P);
 }
 
-// half frames (n_fft 4096 as two P = 64 waves): 512-thread blocks (4 pairs, one
-// block per CU: the per-parity tables take ~145 KB of LDS); SH registers per
-// wave per hop
-template <int SH>
-void launch_half(const MainArgs& A, int ch, hipStream_t s) {
-  const int gm = A.n_rows_lds > 0 ? (A.lds_mixed ? 2 : 1) : 0;
-  const dim3 g((A.n_runs + 3) / 4), b(512);
-#define TM_LAUNCH_H(CHv, GMv) \
-  hipLaunchKernelGGL((k_stft_ola<64, 32, SH, CHv, GMv, false, true, 512, true>), g, b, 0, s, A)
-#ifdef TM_DEV_ONLY_HALF_8
-  (void)gm, (void)ch;
-  TM_LAUNCH_H(2, 1);
-#else
-  if (ch == 2) {
-    if (gm == 1) TM_LAUNCH_H(2, 1);
-    else if (gm == 2) TM_LAUNCH_H(2, 2);
-    else TM_LAUNCH_H(2, 0);
-  } else {
-    if (gm == 1) TM_LAUNCH_H(1, 1);
-    else if (gm == 2) TM_LAUNCH_H(1, 2);
-    else TM_LAUNCH_H(1, 0);
-  }
-#endif
-#undef TM_LAUNCH_H
-}
-
 void launch_transform(const MainArgs& A, int P, int NR, int SH, int ch, int wg, hipStream_t s) {
-#if defined(TM_DEV_ONLY_HALF_8)  // development builds: the half-frame 4096/1024 kernel only
-  (void)P, (void)NR, (void)SH, (void)wg;
-  launch_half<8>(A, ch, s);
-#elif defined(TM_DEV_ONLY_2048_512)  // development builds: the headline configuration only
+#ifdef TM_DEV_ONLY_2048_512  // development builds: the headline configuration only
   if (P == 64 && SH == 8) launch_main<64, 32, 8>(A, ch, wg, s);
 #else
-  if (A.half) {
-    if (SH == 4) launch_half<4>(A, ch, s);
-    else if (SH == 8) launch_half<8>(A, ch, s);
-    else launch_half<16>(A, ch, s);
-    return;
-  }
   if (P == 64) {
     if (SH == 4) launch_main<64, 32, 4>(A, ch, wg, s);
     else if (SH == 8) launch_main<64, 32, 8>(A, ch, wg, s);
@@ -1214,13 +1069,8 @@ void launch_frames(const MainArgs& A, int P, int NR, int blocks, hipStream_t s) 
 }
 
 void launch_gain_perm(int P, int NR, const float* gains, int n_rows, int n_bins, float* out,
-                      hipStream_t s, int half) {
+                      hipStream_t s) {
   const int N = P * NR;
-  if (half) {
-    hipLaunchKernelGGL(k_gain_perm_h, dim3((n_rows * N + 255) / 256), dim3(256), 0, s, gains, n_rows,
-                       n_bins, out);
-    return;
-  }
   const int nb = (n_rows * N + 255) / 256;
   if (P == 64)
     hipLaunchKernelGGL((k_gain_perm<64, 32>), dim3(nb), dim3(256), 0, s, gains, n_rows, n_bins, out);
