@@ -2298,7 +2298,6 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
   A.chunk_rng = p->chunk_rng;
   A.err = p->err;
   A.lim_spin = p->lim_spin;
-  A.lim_rev = env_int("TOMATIS_LIM_REV", 0);
   A.prof = nullptr;
   if (limit > 0.f) {
     if (!p->chunk_done) return TOMATIS_E_UNSUPPORTED;

@@ -56,7 +56,6 @@ struct MainArgs {
   const int64_t* chunk_rng;  // [2 * chunk]: output-relative [p0, p1)
   uint32_t* err;        // TOMATIS_ERR_* bits
   int lim_spin;         // fused-limiter wait bound (polls of the chunk counter)
-  int lim_rev;          // rescale newest output first (TOMATIS_LIM_REV)
   unsigned long long* prof;  // TM_PROFILE builds only: per-phase wave cycles
 };
 

@@ -116,10 +116,7 @@ __device__ void limit_own(const MainArgs& A, const TomatisStream& S, int gc, int
   f4v* b4 = reinterpret_cast<f4v*>(base);
   const int64_t n4 = n >> 2;
   constexpr int U = 16;
-  // blocks of 64 U float4 (A.lim_rev: newest first, while the MALL still holds it)
-  const int64_t nb = (n4 + 64 * U - 1) / (64 * U);
-  for (int64_t j = 0; j < nb; ++j) {
-    const int64_t i = (A.lim_rev ? nb - 1 - j : j) * (64 * U) + lane;
+  for (int64_t i = lane; i < n4; i += 64 * U) {
     f4v t[U];
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -591,8 +588,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
     const int nw = P / 64, w = L >> 6;
     const int64_t span = hi - lo, per = (span + nw - 1) / nw;
     const int64_t wlo = lo + per * w, whi = min(hi, wlo + per);
-    for (int cc = cid_first; cc <= cid; ++cc) {
-      const int c = A.lim_rev ? cid + cid_first - cc : cc;
+    for (int c = cid_first; c <= cid; ++c) {
       // edge chunks (shared with a neighbouring time shard) are scaled after
       // the peak exchange instead (tomatis_apply_limiter_edges)
       if (((A.edge_mask & 1) && c == 0) || ((A.edge_mask & 2) && c == S.n_chunks - 1)) continue;
