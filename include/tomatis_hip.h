@@ -298,7 +298,10 @@ int tomatis_synth_fill(float* x, int64_t n, int32_t ch, int32_t sr, uint32_t see
 /* ---------------------------------------------------------------------------
  * Analysis spectra (tm_analysis.hip).  Frames
  * f = 0 .. F-1 start at sample f*hop, F = 1 + (n - n_fft) / hop (n >= n_fft);
- * n_fft a power of two in [256, 8192]; x (and y) float32 [n][ch] interleaved.
+ * x (and y) float32 [n][ch] interleaved.  n_fft: spectra take powers of two
+ * in [16, 16384] and other lengths in [16, 8192] (Bluestein's chirp-z over a
+ * power of two >= 2 n_fft - 1, in LDS); tomatis_an_frame_r any n_fft in
+ * [1, 16384].  Outside: TOMATIS_E_UNSUPPORTED.
  * ------------------------------------------------------------------------- */
 #define TOMATIS_AN_LEVEL_CHMEAN 0     /* mono = sqrt(mean_c x_c^2)        validate_layer1.py:304-306 */
 #define TOMATIS_AN_LEVEL_POWER_MONO 1 /* mono = sqrt(0.5(L^2+R^2)+1e-12)  layer2_analyze_eq.py:71, compare_audio.py:7-10 */
@@ -349,7 +352,7 @@ int tomatis_an_frame_median(const float* spec, int32_t n_frames, int32_t n_bins,
 /* Per-frame band energies of rfft(win * power_mono(x)) for stereo x
  * (stft_band_tilt, calibrate_to_baseline_v2.py:17-31): out[f][0] = sum of the
  * float32 power re^2+im^2 over bins [lo0, lo1), out[f][1] over [hi0, hi1).
- * Frames as tomatis_an_spectra; n_fft a power of two in [256, 8192]. */
+ * Frames and n_fft as tomatis_an_spectra. */
 int tomatis_an_band_energy(const float* x, int64_t n, int32_t n_fft, int32_t hop,
                            int32_t lo0, int32_t lo1, int32_t hi0, int32_t hi1,
                            const float* win, float* out, void* hip_stream);

@@ -21,6 +21,19 @@ AN_CASES = [
          N=44100 * 6 + 333, seed=35, n_fft=2048, hop=512, level_threshold=-60.0),
     dict(name="an_cond_48k_mono_4096_1024", fn="compute_conditional_spectrum", sr=48000, ch=1,
          N=48000 * 6 + 9, seed=36, n_fft=4096, hop=1024, level_threshold=-50.0),
+    # any n_fft (round 3): Bluestein lengths and 16384 / tiny frames
+    dict(name="an_mag_48k_3000_750", fn="stft_mag_avg", sr=48000, ch=2, N=48000 * 4 + 123,
+         seed=41, n_fft=3000, hop=750),
+    dict(name="an_mag_44k_16384_4096", fn="stft_mag_avg", sr=44100, ch=2, N=44100 * 4 + 5,
+         seed=42, n_fft=16384, hop=4096),
+    dict(name="an_mag_48k_100_37", fn="stft_mag_avg", sr=48000, ch=2, N=48000 + 3,
+         seed=43, n_fft=100, hop=37),
+    dict(name="an_logpow_48k_6000_1500", fn="stft_logpower_median", sr=48000, ch=2,
+         N=48000 * 8 + 71, seed=44, n_fft=6000, hop=1500, music_dbfs=-65.0),
+    dict(name="an_cond_44k_st_1500_375", fn="compute_conditional_spectrum", sr=44100, ch=2,
+         N=44100 * 6 + 1, seed=45, n_fft=1500, hop=375, level_threshold=-60.0),
+    dict(name="an_cond_48k_mono_1000_250", fn="compute_conditional_spectrum", sr=48000, ch=1,
+         N=48000 * 5 + 17, seed=46, n_fft=1000, hop=250, level_threshold=-50.0),
 ]
 AN_BY_NAME = {c["name"]: c for c in AN_CASES}
 

@@ -5,7 +5,10 @@
   device FFT is this build's own, pocketfft's rounding differs by ~1e-7 rel.);
 * the exact pieces bit-for-bit vs the oracle / numpy: per-frame r (numpy
   pairwise order), the level-gated frame masks, the median over frames
-  (np.median, both parities, negatives, ties, masks) and the mean over frames.
+  (np.median, both parities, negatives, ties, masks) and the mean over frames;
+* any n_fft (Bluestein lengths, 16384, tiny frames): reference goldens at
+  3000/1000/1500/6000/100/16384, bit-exact r for numpy's tree at any length,
+  band tilts vs the reference formula, and the size bounds.
 """
 import json
 import os
@@ -66,7 +69,11 @@ def test_device_vs_reference(an, c):
 
 @pytest.mark.parametrize("n_fft,hop,ch,mode", [(2048, 512, 2, 0), (4096, 1024, 1, 0),
                                                 (8192, 4096, 2, 1), (256, 100, 2, 1),
-                                                (1024, 300, 2, 0)])
+                                                (1024, 300, 2, 0),
+                                                # numpy's tree for any length (program)
+                                                (3000, 750, 2, 0), (12000, 3000, 2, 1),
+                                                (16384, 4096, 1, 0), (100, 30, 2, 1),
+                                                (16, 5, 1, 0), (1500, 375, 1, 0)])
 def test_frame_r_bit_exact(an, n_fft, hop, ch, mode):
     from tomatis_audio_processor_amd.synth import synth_stream
     x = synth_stream(40 + n_fft, n_fft * 7 + 3 * hop + 11, ch, 48000)
@@ -130,3 +137,43 @@ def test_errors_like_reference(an):
         an.stft_logpower_median(x, 48000, 2048, 512, -65.0)
     with pytest.raises(ValueError):
         an.stft_mag_avg(np.zeros(100, np.float32), 48000, 4096, 2048)
+
+
+@pytest.mark.parametrize("n_fft,hop", [(3000, 1500), (1000, 250), (16384, 8192), (100, 50)])
+def test_band_tilts_any_n_fft(n_fft, hop):
+    """calibrate_to_baseline_v2.stft_band_tilt (:17-31) per frame at lengths the
+    calibration golden does not use (Bluestein / 16384), against that formula in
+    numpy (pocketfft, float32 P, float sums)."""
+    import torch
+    assert torch.cuda.is_available()
+    from tomatis_audio_processor_amd import calibrate_to_baseline_v2 as cal
+    from tomatis_audio_processor_amd.synth import synth_stream
+    sr = 48000
+    x = synth_stream(90 + n_fft, 8 * n_fft + 3 * hop + 5, 2, sr)
+    got = cal.band_tilts(x, sr, n_fft, hop)
+    F = 1 + (len(x) - n_fft) // hop
+    win = np.hanning(n_fft).astype(np.float32)
+    freqs = np.fft.rfftfreq(n_fft, 1 / sr)
+    lo = (freqs >= 200) & (freqs < 1000)
+    hi = (freqs >= 2000) & (freqs < 8000)
+    want = []
+    for f in range(F):
+        X = np.fft.rfft(orc.power_mono(x[f * hop:f * hop + n_fft]) * win)
+        P = (X.real * X.real + X.imag * X.imag).astype(np.float32)
+        elo, ehi = float(np.sum(P[lo]) + 1e-12), float(np.sum(P[hi]) + 1e-12)
+        want.append(10 * np.log10(ehi / elo + 1e-12))
+    want = np.asarray(want, np.float32)
+    assert got.shape == want.shape
+    assert float(np.abs(got - want).max()) < 1e-3
+
+
+def test_n_fft_bounds(an):
+    """Any n_fft np.fft.rfft takes within the LDS: powers of two 16..16384,
+    other lengths 16..8192 (Bluestein over >= 2n - 1 points); outside that the
+    wrappers refuse before any launch."""
+    x = np.zeros((48000, 2), np.float32)
+    for bad in (8, 15, 8193, 9000, 32768):
+        with pytest.raises(ValueError, match="n_fft"):
+            an.stft_mag_avg(x[:, 0], 48000, bad, bad // 2)
+    assert an.stft_mag_avg(x[:, 0], 48000, 16, 8).shape == (9,)
+    assert an.stft_mag_avg(x[:, 0], 48000, 8191, 4000).shape == (4096,)

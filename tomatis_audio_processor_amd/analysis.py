@@ -30,7 +30,9 @@ EPS = 1e-12
 AN_LEVEL_CHMEAN, AN_LEVEL_POWER_MONO = 0, 1
 AN_SIG_RAW, AN_SIG_POWER_MONO = 0, 1
 AN_MAG, AN_LOGPOW, AN_RATIO = 0, 1, 2
-MAX_N_FFT = 8192
+MIN_N_FFT = 16               # tm_analysis.hip kMinN
+MAX_N_FFT = 16384            # kMaxM: one FFT in LDS
+MAX_N_FFT_BLUESTEIN = 8192   # 2 n_fft - 1 <= kMaxM
 
 
 def _torch():
@@ -53,8 +55,14 @@ def _dev(a, ch=None):
 
 
 def _check_n_fft(n_fft):
-    if n_fft < 256 or n_fft > MAX_N_FFT or (n_fft & (n_fft - 1)):
-        raise ValueError(f"n_fft must be a power of two in [256, {MAX_N_FFT}], got {n_fft}")
+    """Any length np.fft.rfft takes, within the LDS: powers of two in
+    [16, MAX_N_FFT], other lengths in [16, MAX_N_FFT_BLUESTEIN] (Bluestein's
+    chirp-z runs a power-of-two FFT of >= 2 n_fft - 1 points)."""
+    pow2 = n_fft > 0 and (n_fft & (n_fft - 1)) == 0
+    cap = MAX_N_FFT if pow2 else MAX_N_FFT_BLUESTEIN
+    if n_fft < MIN_N_FFT or n_fft > cap:
+        raise ValueError(f"n_fft={n_fft}: the analysis kernels take {MIN_N_FFT} <= n_fft <= "
+                         f"{cap} ({'power of two' if pow2 else 'Bluestein'}), as tm_analysis.hip")
 
 
 def _n_frames(n, n_fft, hop):

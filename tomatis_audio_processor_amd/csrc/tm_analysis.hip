@@ -25,11 +25,16 @@
 //    the hop-strided PCM), Stockham autosort FFT in LDS (one radix-2 stage when
 //    log2 n is odd, then radix-4 stages; every stage reads its butterflies into
 //    registers, barrier, writes, barrier), twiddles from a float table built in
-//    double precision once per n_fft.  Output rows [F][n/2+1] f32.
+//    double precision once per size.  Any n_fft >= 16 (as np.fft.rfft): powers
+//    of two up to 16384 directly, other lengths up to 8192 by Bluestein's
+//    chirp-z over M = 2^k >= 2n - 1 in the same LDS buffer (tlds::lds_dft,
+//    tables per n from tm_host_dsp.h).  Output rows [F][n/2+1] f32.
 //  * k_an_frame_r: numpy's pairwise mean of m^2 per frame, restated exactly
 //    (128-sample leaves of 8 sequential chains, fixed 8-chain tree, perfect tree
 //    over leaves; correctly rounded sqrtf, -ffp-contract=off) so level gating is
-//    decided on the bit pattern of r, like the processors' gate.
+//    decided on the bit pattern of r, like the processors' gate.  Other frame
+//    lengths take k_an_frame_r_pw: numpy's tree for that length (leaves +
+//    postfix program, NPY_BUFSIZE chunks) built on the host.
 //  * median: per-bin radix select over the frame axis on order-preserving u32
 //    keys, 8-bit digits, 4 passes (+1 min pass for even counts); each pass is a
 //    grid of (64-bin group x frame split) workgroups building LDS histograms
@@ -43,24 +48,32 @@
 #include <algorithm>
 #include <map>
 #include <mutex>
+#include <type_traits>
+#include <vector>
 
 #include "../../include/tomatis_hip.h"
+#include "tm_host_dsp.h"
 #include "tm_lds_fft.h"
 
 namespace {
 
 constexpr int kT = 256;                // threads per spectrum workgroup
-constexpr int kMaxN = 8192;            // largest n_fft
+constexpr int kMaxTreeN = 8192;        // k_an_frame_r: powers of two in [256, 8192]
+constexpr int kMaxM = 16384;           // largest FFT in LDS (128 KiB of float2)
+constexpr int kMinN = 16;              // smallest spectrum n_fft
+constexpr int kPwMax = 256;            // k_an_frame_r_pw leaves (n_fft <= 16384)
 constexpr float kEps = 1e-12f;
 
 int an_fail(hipError_t e) { return e == hipSuccess ? TOMATIS_OK : TOMATIS_E_HIP; }
 int an_launch() { return an_fail(hipGetLastError()); }
 
-int ilog2_pow2(int n) {
-  if (n <= 0 || (n & (n - 1))) return -1;
-  int l = 0;
-  while ((1 << l) < n) ++l;
-  return l;
+bool is_pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
+
+// FFT size in LDS for a length-n DFT (0: unsupported)
+int dft_m(int n) {
+  if (n < kMinN) return 0;
+  const int M = is_pow2(n) ? n : thost::bluestein_m(n);
+  return M <= kMaxM ? M : 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -76,6 +89,75 @@ __global__ void k_an_twiddle(float2* tw, int n) {
 
 std::mutex g_tw_mu;
 std::map<std::pair<int, int>, float2*> g_tw;  // (device, n) -> table (process lifetime)
+
+template <typename T>
+int upload(const std::vector<T>& v, T** out) {
+  T* p = nullptr;
+  if (hipMalloc(&p, sizeof(T) * v.size()) != hipSuccess) return TOMATIS_E_NOMEM;
+  if (hipMemcpy(p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(p);
+    return TOMATIS_E_HIP;
+  }
+  *out = p;
+  return TOMATIS_OK;
+}
+
+struct Chirp {  // Bluestein tables for one n (tm_host_dsp.h bluestein_tables)
+  float2* b = nullptr;
+  float2* h = nullptr;
+};
+std::map<std::pair<int, int>, Chirp> g_chirp;  // (device, n), process lifetime
+
+int chirp_tables(int n, int M, Chirp* out) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return TOMATIS_E_HIP;
+  std::lock_guard<std::mutex> lk(g_tw_mu);
+  auto it = g_chirp.find({dev, n});
+  if (it != g_chirp.end()) {
+    *out = it->second;
+    return TOMATIS_OK;
+  }
+  std::vector<float2> bf, hf;
+  thost::bluestein_tables(n, M, bf, hf);
+  Chirp c;
+  int rc = upload(bf, &c.b);
+  if (rc == TOMATIS_OK && (rc = upload(hf, &c.h)) != TOMATIS_OK) (void)hipFree(c.b);
+  if (rc != TOMATIS_OK) return rc;
+  g_chirp[{dev, n}] = c;
+  *out = c;
+  return TOMATIS_OK;
+}
+
+struct PwProg {  // numpy's pairwise tree over one frame length
+  int2* leaf = nullptr;
+  int16_t* prog = nullptr;
+  int n_leaf = 0, n_prog = 0;
+};
+std::map<std::pair<int, int>, PwProg> g_pw;  // (device, n), process lifetime
+
+int pw_program(int n, PwProg* out) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return TOMATIS_E_HIP;
+  std::lock_guard<std::mutex> lk(g_tw_mu);
+  auto it = g_pw.find({dev, n});
+  if (it != g_pw.end()) {
+    *out = it->second;
+    return TOMATIS_OK;
+  }
+  std::vector<int2> lv;
+  std::vector<int16_t> prog;
+  thost::pw_program(n, lv, prog);
+  if ((int)lv.size() > kPwMax) return TOMATIS_E_UNSUPPORTED;
+  PwProg q;
+  q.n_leaf = (int)lv.size();
+  q.n_prog = (int)prog.size();
+  int rc = upload(lv, &q.leaf);
+  if (rc == TOMATIS_OK && (rc = upload(prog, &q.prog)) != TOMATIS_OK) (void)hipFree(q.leaf);
+  if (rc != TOMATIS_OK) return rc;
+  g_pw[{dev, n}] = q;
+  *out = q;
+  return TOMATIS_OK;
+}
 
 int twiddles(int n, hipStream_t s, const float2** out) {
   int dev = 0;
@@ -133,7 +215,7 @@ template <int MODE, int CH>  // MODE: TOMATIS_AN_LEVEL_CHMEAN / _POWER_MONO
 __global__ __launch_bounds__(256) void k_an_frame_r(const float* __restrict__ x, int n_fft,
                                                     int hop, int n_frames, float sc,
                                                     float* __restrict__ r_out) {
-  __shared__ float lv[4][kMaxN / 128];
+  __shared__ float lv[4][kMaxTreeN / 128];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int f = blockIdx.x * 4 + w;
   const bool live = f < n_frames;  // wave-uniform
@@ -172,6 +254,67 @@ __global__ __launch_bounds__(256) void k_an_frame_r(const float* __restrict__ x,
   }
 }
 
+// any frame length: numpy's pairwise tree from the host program (leaf >= 0
+// pushes that leaf's sum, -1 adds the top two); leaves follow numpy's block rule
+// (sequential below 8, else 8 accumulators + fixed tree + sequential remainder)
+template <int MODE, int CH>
+__device__ __forceinline__ float m2_at(const float* __restrict__ x, int64_t p, float sc) {
+  if constexpr (MODE == TOMATIS_AN_LEVEL_POWER_MONO) {
+    const float m = power_mono(x, p, sc);
+    return m * m;
+  } else {
+    return m2_chmean<CH>(x, p, sc);
+  }
+}
+
+template <int MODE, int CH>
+__global__ __launch_bounds__(256) void k_an_frame_r_pw(const float* __restrict__ x, int n_fft,
+                                                       int hop, float sc,
+                                                       const int2* __restrict__ leaf, int n_leaf,
+                                                       const int16_t* __restrict__ prog,
+                                                       int n_prog, float* __restrict__ r_out) {
+  __shared__ float ls[kPwMax];
+  const int f = blockIdx.x;
+  const int64_t p0 = (int64_t)f * hop;
+  for (int l = threadIdx.x; l < n_leaf; l += blockDim.x) {
+    const int2 lf = leaf[l];
+    const int64_t q = p0 + lf.x;
+    const int len = lf.y;
+    float res;
+    if (len < 8) {
+      res = 0.f;
+      for (int i = 0; i < len; ++i) res = res + m2_at<MODE, CH>(x, q + i, sc);
+    } else {
+      float r[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = m2_at<MODE, CH>(x, q + j, sc);
+      int i = 8;
+      for (; i < len - (len % 8); i += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] = r[j] + m2_at<MODE, CH>(x, q + i + j, sc);
+      }
+      res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+      for (; i < len; ++i) res = res + m2_at<MODE, CH>(x, q + i, sc);
+    }
+    ls[l] = res;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float stk[32];
+    int sp = 0;
+    for (int i = 0; i < n_prog; ++i) {
+      const int op = prog[i];
+      if (op >= 0) {
+        stk[sp++] = ls[op];
+      } else {
+        const float b = stk[--sp];
+        stk[sp - 1] = stk[sp - 1] + b;
+      }
+    }
+    r_out[f] = sqrtf(stk[0] / (float)n_fft + kEps);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // frame selection on r bit patterns (exact level predicates, dsp.gate_bits)
 // ---------------------------------------------------------------------------
@@ -203,7 +346,7 @@ __global__ __launch_bounds__(256) void k_an_select(const float* __restrict__ r, 
 using tlds::cadd;
 using tlds::cmul;
 using tlds::csub;
-using tlds::lds_fft;
+using tlds::lds_dft;
 
 // ---------------------------------------------------------------------------
 // spectra
@@ -212,9 +355,11 @@ struct SpecArgs {
   const float* x;
   const float* y;
   const float* win;
-  const float2* tw;
+  const float2* tw;  // exp(-2 pi i t / M)
+  const float2* bb;  // Bluestein chirp b (n_fft), BLUE kernels only
+  const float2* bh;  // Bluestein kernel spectrum H (M)
   float* out;
-  int n_fft, logn, hop, n_frames, n_bins;
+  int n_fft, M, hop, n_frames, n_bins;
   float sc;
   int band[4];  // TOMATIS_AN_BAND: bins [band0, band1) and [band2, band3)
 };
@@ -225,13 +370,16 @@ __device__ __forceinline__ float sig_at(const float* __restrict__ x, int64_t p, 
   else return x[p] * sc;
 }
 
+// DFT bin mirrored for the two-real-frames split: (n - k) mod n
+__device__ __forceinline__ int mirror(int k, int n) { return k == 0 ? 0 : n - k; }
+
 // MAG / LOGPOW: workgroup per frame pair (2g, 2g+1) packed as a + ib
-template <int KIND, int SIG, int N>
+template <int KIND, int SIG, int M, bool BLUE>
 __global__ __launch_bounds__(kT) void k_an_spec_pair(SpecArgs A) {
-  __shared__ float2 buf[N];
+  __shared__ float2 buf[M];
   const int f0 = blockIdx.x * 2, f1 = f0 + 1;
   const bool has1 = f1 < A.n_frames;
-  constexpr int n = N;
+  const int n = A.n_fft;
   const int64_t p0 = (int64_t)f0 * A.hop, p1 = (int64_t)f1 * A.hop;
   for (int i = threadIdx.x; i < n; i += kT) {
     const float w = A.win[i];
@@ -240,11 +388,11 @@ __global__ __launch_bounds__(kT) void k_an_spec_pair(SpecArgs A) {
     buf[i] = make_float2(a, b);
   }
   __syncthreads();
-  lds_fft<N>(buf, A.tw);
+  lds_dft<M, BLUE>(buf, n, A.tw, A.bb, A.bh);
   float* o0 = A.out + (int64_t)f0 * A.n_bins;
   float* o1 = A.out + (int64_t)f1 * A.n_bins;
   for (int k = threadIdx.x; k < A.n_bins; k += kT) {
-    const float2 zk = buf[k], zm = buf[(n - k) & (n - 1)];
+    const float2 zk = buf[k], zm = buf[mirror(k, n)];
     // A = (Z[k] + conj Z[n-k]) / 2, B = (Z[k] - conj Z[n-k]) / 2i
     const float2 fa = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
     const float2 fb = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
@@ -265,9 +413,10 @@ __global__ __launch_bounds__(kT) void k_an_spec_pair(SpecArgs A) {
 // BAND (stft_band_tilt, calibrate_to_baseline_v2.py:17-31): per frame of the
 // pair the float32 power re^2 + im^2 of rfft(win * power_mono) summed over two
 // bin ranges; workgroup per frame pair as k_an_spec_pair, block reduction.
-template <int N>
+template <int M, bool BLUE>
 __global__ __launch_bounds__(kT) void k_an_band_pair(SpecArgs A) {
-  __shared__ float2 buf[N];
+  __shared__ float2 buf[M];
+  const int N = A.n_fft;
   __shared__ float red[kT / 64][4];
   const int f0 = blockIdx.x * 2, f1 = f0 + 1;
   const bool has1 = f1 < A.n_frames;
@@ -279,12 +428,12 @@ __global__ __launch_bounds__(kT) void k_an_band_pair(SpecArgs A) {
     buf[i] = make_float2(a, b);
   }
   __syncthreads();
-  lds_fft<N>(buf, A.tw);
+  lds_dft<M, BLUE>(buf, N, A.tw, A.bb, A.bh);
   float acc[4] = {0.f, 0.f, 0.f, 0.f};  // (frame a, band lo), (a, hi), (b, lo), (b, hi)
   for (int k = threadIdx.x; k < A.n_bins; k += kT) {
     const bool lo = k >= A.band[0] && k < A.band[1], hi = k >= A.band[2] && k < A.band[3];
     if (!lo && !hi) continue;
-    const float2 zk = buf[k], zm = buf[(N - k) & (N - 1)];
+    const float2 zk = buf[k], zm = buf[mirror(k, N)];
     const float2 fa = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
     const float2 fb = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
     const float pa = fa.x * fa.x + fa.y * fa.y, pb = fb.x * fb.x + fb.y * fb.y;
@@ -358,12 +507,12 @@ __global__ __launch_bounds__(256) void k_cal_gate_grid(const float* __restrict__
 }
 
 // RATIO: workgroup per frame; per channel one FFT of x_c + i y_c
-template <int CH, int N>
+template <int CH, int M, bool BLUE>
 __global__ __launch_bounds__(kT) void k_an_spec_ratio(SpecArgs A) {
-  __shared__ float2 buf[N];
-  constexpr int kMaxUB = (N / 2 + 1 + kT - 1) / kT;  // bins per thread
+  __shared__ float2 buf[M];
+  constexpr int kMaxUB = (M / 2 + 1 + kT - 1) / kT;  // bins per thread (n/2+1 <= M/2+1)
   const int f = blockIdx.x;
-  constexpr int n = N;
+  const int n = A.n_fft;
   const int64_t p0 = (int64_t)f * A.hop;
   float ax[kMaxUB], ay[kMaxUB];
 #pragma unroll
@@ -376,12 +525,12 @@ __global__ __launch_bounds__(kT) void k_an_spec_ratio(SpecArgs A) {
       buf[i] = make_float2(A.x[q] * w, A.y[q] * w);
     }
     __syncthreads();
-    lds_fft<N>(buf, A.tw);
+    lds_dft<M, BLUE>(buf, n, A.tw, A.bb, A.bh);
 #pragma unroll
     for (int u = 0; u < kMaxUB; ++u) {
       const int k = threadIdx.x + u * kT;
       if (k < A.n_bins) {
-        const float2 zk = buf[k], zm = buf[(n - k) & (n - 1)];
+        const float2 zk = buf[k], zm = buf[mirror(k, n)];
         const float xr = 0.5f * (zk.x + zm.x), xi = 0.5f * (zk.y - zm.y);
         const float yr = 0.5f * (zk.y + zm.y), yi = -0.5f * (zk.x - zm.x);
         ax[u] = ax[u] + hypotf(xr, xi);  // X += |rfft(x_c * win)|
@@ -542,36 +691,99 @@ __global__ void k_an_med_final(const MedState* __restrict__ st, int n_bins, int 
   out[b] = ((0.f + v1) + v2) / 2.0f;
 }
 
+// SpecArgs' FFT tables for n_fft: M, twiddles of M, Bluestein tables
+int dft_args(int n_fft, hipStream_t s, SpecArgs* A) {
+  A->M = dft_m(n_fft);
+  if (A->M == 0) return TOMATIS_E_UNSUPPORTED;
+  int rc = twiddles(A->M, s, &A->tw);
+  if (rc != TOMATIS_OK || A->M == n_fft) return rc;
+  Chirp c;
+  if ((rc = chirp_tables(n_fft, A->M, &c)) != TOMATIS_OK) return rc;
+  A->bb = c.b;
+  A->bh = c.h;
+  return TOMATIS_OK;
+}
+
+// calls f(integral_constant<M>, bool_constant<BLUE>) for the args' FFT size
+// (M = 16 .. 16384; Bluestein sizes start at M = 32 since n_fft >= 16)
+template <int M, typename L>
+void launch_m(bool blue, L& f) {
+  if constexpr (M >= 32) {
+    if (blue) {
+      f(std::integral_constant<int, M>{}, std::true_type{});
+      return;
+    }
+  }
+  f(std::integral_constant<int, M>{}, std::false_type{});
+}
+
+template <typename L>
+int dispatch_m(const SpecArgs& A, L&& f) {
+  const bool blue = A.M != A.n_fft;
+  switch (A.M) {
+    case 16: launch_m<16>(blue, f); break;
+    case 32: launch_m<32>(blue, f); break;
+    case 64: launch_m<64>(blue, f); break;
+    case 128: launch_m<128>(blue, f); break;
+    case 256: launch_m<256>(blue, f); break;
+    case 512: launch_m<512>(blue, f); break;
+    case 1024: launch_m<1024>(blue, f); break;
+    case 2048: launch_m<2048>(blue, f); break;
+    case 4096: launch_m<4096>(blue, f); break;
+    case 8192: launch_m<8192>(blue, f); break;
+    case 16384: launch_m<16384>(blue, f); break;
+    default: return TOMATIS_E_UNSUPPORTED;
+  }
+  return an_launch();
+}
+
 }  // namespace
 
 extern "C" {
 
 int tomatis_an_frame_r(const float* x, int64_t n, int32_t ch, int32_t n_fft, int32_t hop,
                        int32_t level_mode, float scale, float* r_out, void* hs) {
-  const int logn = ilog2_pow2(n_fft);
-  if (!x || !r_out || hop < 1 || ch < 1) return TOMATIS_E_ARG;
-  if (logn < 8 || n_fft > kMaxN) return TOMATIS_E_UNSUPPORTED;
-  if (n < n_fft) return TOMATIS_OK;
-  const int64_t F = 1 + (n - n_fft) / hop;
-  if (F > INT32_MAX) return TOMATIS_E_UNSUPPORTED;
-  const dim3 g((unsigned)((F + 3) / 4));
-  hipStream_t s = (hipStream_t)hs;
+  if (!x || !r_out || hop < 1 || ch < 1 || n_fft < 1) return TOMATIS_E_ARG;
+  if (n_fft > kMaxM) return TOMATIS_E_UNSUPPORTED;
   if (level_mode == TOMATIS_AN_LEVEL_POWER_MONO) {
     if (ch != 2) return TOMATIS_E_ARG;
-    hipLaunchKernelGGL((k_an_frame_r<TOMATIS_AN_LEVEL_POWER_MONO, 2>), g, dim3(256), 0, s, x,
-                       n_fft, hop, (int)F, scale, r_out);
   } else if (level_mode == TOMATIS_AN_LEVEL_CHMEAN) {
-    if (ch == 1)
-      hipLaunchKernelGGL((k_an_frame_r<TOMATIS_AN_LEVEL_CHMEAN, 1>), g, dim3(256), 0, s, x,
-                         n_fft, hop, (int)F, scale, r_out);
-    else if (ch == 2)
-      hipLaunchKernelGGL((k_an_frame_r<TOMATIS_AN_LEVEL_CHMEAN, 2>), g, dim3(256), 0, s, x,
-                         n_fft, hop, (int)F, scale, r_out);
-    else
-      return TOMATIS_E_UNSUPPORTED;
+    if (ch != 1 && ch != 2) return TOMATIS_E_UNSUPPORTED;
   } else {
     return TOMATIS_E_ARG;
   }
+  if (n < n_fft) return TOMATIS_OK;
+  const int64_t F = 1 + (n - n_fft) / hop;
+  if (F > INT32_MAX) return TOMATIS_E_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)hs;
+  const bool pm = level_mode == TOMATIS_AN_LEVEL_POWER_MONO;
+  if (is_pow2(n_fft) && n_fft >= 256 && n_fft <= kMaxTreeN) {
+    // perfect tree over 128-sample leaves
+    const dim3 g((unsigned)((F + 3) / 4));
+    if (pm)
+      hipLaunchKernelGGL((k_an_frame_r<TOMATIS_AN_LEVEL_POWER_MONO, 2>), g, dim3(256), 0, s, x,
+                         n_fft, hop, (int)F, scale, r_out);
+    else if (ch == 1)
+      hipLaunchKernelGGL((k_an_frame_r<TOMATIS_AN_LEVEL_CHMEAN, 1>), g, dim3(256), 0, s, x,
+                         n_fft, hop, (int)F, scale, r_out);
+    else
+      hipLaunchKernelGGL((k_an_frame_r<TOMATIS_AN_LEVEL_CHMEAN, 2>), g, dim3(256), 0, s, x,
+                         n_fft, hop, (int)F, scale, r_out);
+    return an_launch();
+  }
+  PwProg q;
+  int rc = pw_program(n_fft, &q);
+  if (rc != TOMATIS_OK) return rc;
+  const dim3 g((unsigned)F);
+  if (pm)
+    hipLaunchKernelGGL((k_an_frame_r_pw<TOMATIS_AN_LEVEL_POWER_MONO, 2>), g, dim3(256), 0, s, x,
+                       n_fft, hop, scale, q.leaf, q.n_leaf, q.prog, q.n_prog, r_out);
+  else if (ch == 1)
+    hipLaunchKernelGGL((k_an_frame_r_pw<TOMATIS_AN_LEVEL_CHMEAN, 1>), g, dim3(256), 0, s, x,
+                       n_fft, hop, scale, q.leaf, q.n_leaf, q.prog, q.n_prog, r_out);
+  else
+    hipLaunchKernelGGL((k_an_frame_r_pw<TOMATIS_AN_LEVEL_CHMEAN, 2>), g, dim3(256), 0, s, x,
+                       n_fft, hop, scale, q.leaf, q.n_leaf, q.prog, q.n_prog, r_out);
   return an_launch();
 }
 
@@ -595,58 +807,58 @@ int tomatis_an_select(const float* r, int32_t n_frames, uint32_t thr_bits,
 int tomatis_an_spectra(const float* x, const float* y, int64_t n, int32_t ch, int32_t n_fft,
                        int32_t hop, int32_t kind, int32_t sig_mode, float scale,
                        const float* win, float* out, void* hs) {
-  const int logn = ilog2_pow2(n_fft);
-  if (!x || !win || !out || hop < 1 || ch < 1) return TOMATIS_E_ARG;
-  if (logn < 8 || n_fft > kMaxN) return TOMATIS_E_UNSUPPORTED;
+  if (!x || !win || !out || hop < 1 || ch < 1 || n_fft < 1) return TOMATIS_E_ARG;
+  if (dft_m(n_fft) == 0) return TOMATIS_E_UNSUPPORTED;
+  if (kind == TOMATIS_AN_RATIO) {
+    if (!y) return TOMATIS_E_ARG;
+    if (ch != 1 && ch != 2) return TOMATIS_E_UNSUPPORTED;
+  } else if (kind == TOMATIS_AN_MAG || kind == TOMATIS_AN_LOGPOW) {
+    if (sig_mode == TOMATIS_AN_SIG_RAW) {
+      if (ch != 1) return TOMATIS_E_ARG;
+    } else if (sig_mode == TOMATIS_AN_SIG_POWER_MONO) {
+      if (ch != 2) return TOMATIS_E_ARG;
+    } else {
+      return TOMATIS_E_ARG;
+    }
+  } else {
+    return TOMATIS_E_ARG;
+  }
   if (n < n_fft) return TOMATIS_OK;
   const int64_t F = 1 + (n - n_fft) / hop;
   if (F > INT32_MAX) return TOMATIS_E_UNSUPPORTED;
   hipStream_t s = (hipStream_t)hs;
-  SpecArgs A{x, y, win, nullptr, out, n_fft, logn, hop, (int)F, n_fft / 2 + 1, scale};
-  int rc = twiddles(n_fft, s, &A.tw);
+  SpecArgs A{x, y, win, nullptr, nullptr, nullptr, out, n_fft, 0, hop, (int)F, n_fft / 2 + 1,
+             scale};
+  int rc = dft_args(n_fft, s, &A);
   if (rc != TOMATIS_OK) return rc;
   if (kind == TOMATIS_AN_RATIO) {
-    if (!y) return TOMATIS_E_ARG;
-    if (ch != 1 && ch != 2) return TOMATIS_E_UNSUPPORTED;
     const dim3 g((unsigned)F);
-#define AN_RATIO(NN)                                                                 \
-  if (n_fft == NN) {                                                                 \
-    if (ch == 1) hipLaunchKernelGGL((k_an_spec_ratio<1, NN>), g, dim3(kT), 0, s, A); \
-    else hipLaunchKernelGGL((k_an_spec_ratio<2, NN>), g, dim3(kT), 0, s, A);         \
-  }
-    AN_RATIO(256) AN_RATIO(512) AN_RATIO(1024) AN_RATIO(2048) AN_RATIO(4096) AN_RATIO(8192)
-#undef AN_RATIO
-    return an_launch();
-  }
-  if (kind != TOMATIS_AN_MAG && kind != TOMATIS_AN_LOGPOW) return TOMATIS_E_ARG;
-  if (sig_mode == TOMATIS_AN_SIG_RAW) {
-    if (ch != 1) return TOMATIS_E_ARG;
-  } else if (sig_mode == TOMATIS_AN_SIG_POWER_MONO) {
-    if (ch != 2) return TOMATIS_E_ARG;
-  } else {
-    return TOMATIS_E_ARG;
+    return dispatch_m(A, [&](auto m, auto b) {
+      constexpr int MM = decltype(m)::value;
+      constexpr bool BL = decltype(b)::value;
+      if (ch == 1) hipLaunchKernelGGL((k_an_spec_ratio<1, MM, BL>), g, dim3(kT), 0, s, A);
+      else hipLaunchKernelGGL((k_an_spec_ratio<2, MM, BL>), g, dim3(kT), 0, s, A);
+    });
   }
   const dim3 g((unsigned)((F + 1) / 2));
-#define AN_PAIR_N(K, S, NN) \
-  if (kind == K && sig_mode == S && n_fft == NN) hipLaunchKernelGGL((k_an_spec_pair<K, S, NN>), g, dim3(kT), 0, s, A);
-#define AN_PAIR(K, S) \
-  AN_PAIR_N(K, S, 256) AN_PAIR_N(K, S, 512) AN_PAIR_N(K, S, 1024) AN_PAIR_N(K, S, 2048) \
-  AN_PAIR_N(K, S, 4096) AN_PAIR_N(K, S, 8192)
-  AN_PAIR(TOMATIS_AN_MAG, TOMATIS_AN_SIG_RAW)
-  AN_PAIR(TOMATIS_AN_MAG, TOMATIS_AN_SIG_POWER_MONO)
-  AN_PAIR(TOMATIS_AN_LOGPOW, TOMATIS_AN_SIG_RAW)
-  AN_PAIR(TOMATIS_AN_LOGPOW, TOMATIS_AN_SIG_POWER_MONO)
-#undef AN_PAIR
-#undef AN_PAIR_N
-  return an_launch();
+  const bool raw = sig_mode == TOMATIS_AN_SIG_RAW;
+  return dispatch_m(A, [&](auto m, auto b) {
+    constexpr int MM = decltype(m)::value;
+    constexpr bool BL = decltype(b)::value;
+    constexpr int MAG = TOMATIS_AN_MAG, LOGP = TOMATIS_AN_LOGPOW;
+    constexpr int RAW = TOMATIS_AN_SIG_RAW, PM = TOMATIS_AN_SIG_POWER_MONO;
+    if (kind == MAG && raw) hipLaunchKernelGGL((k_an_spec_pair<MAG, RAW, MM, BL>), g, dim3(kT), 0, s, A);
+    else if (kind == MAG) hipLaunchKernelGGL((k_an_spec_pair<MAG, PM, MM, BL>), g, dim3(kT), 0, s, A);
+    else if (raw) hipLaunchKernelGGL((k_an_spec_pair<LOGP, RAW, MM, BL>), g, dim3(kT), 0, s, A);
+    else hipLaunchKernelGGL((k_an_spec_pair<LOGP, PM, MM, BL>), g, dim3(kT), 0, s, A);
+  });
 }
 
 int tomatis_an_band_energy(const float* x, int64_t n, int32_t n_fft, int32_t hop,
                            int32_t lo0, int32_t lo1, int32_t hi0, int32_t hi1,
                            const float* win, float* out, void* hs) {
-  const int logn = ilog2_pow2(n_fft);
-  if (!x || !win || !out || hop < 1) return TOMATIS_E_ARG;
-  if (logn < 8 || n_fft > kMaxN) return TOMATIS_E_UNSUPPORTED;
+  if (!x || !win || !out || hop < 1 || n_fft < 1) return TOMATIS_E_ARG;
+  if (dft_m(n_fft) == 0) return TOMATIS_E_UNSUPPORTED;
   const int nb = n_fft / 2 + 1;
   if (lo0 < 0 || lo1 < lo0 || lo1 > nb || hi0 < 0 || hi1 < hi0 || hi1 > nb) return TOMATIS_E_ARG;
   if (lo1 > hi0 && hi1 > lo0) return TOMATIS_E_ARG;  // bands must not overlap
@@ -654,16 +866,15 @@ int tomatis_an_band_energy(const float* x, int64_t n, int32_t n_fft, int32_t hop
   const int64_t F = 1 + (n - n_fft) / hop;
   if (F > INT32_MAX) return TOMATIS_E_UNSUPPORTED;
   hipStream_t s = (hipStream_t)hs;
-  SpecArgs A{x, nullptr, win, nullptr, out, n_fft, logn, hop, (int)F, nb, 1.0f,
+  SpecArgs A{x, nullptr, win, nullptr, nullptr, nullptr, out, n_fft, 0, hop, (int)F, nb, 1.0f,
              {lo0, lo1, hi0, hi1}};
-  int rc = twiddles(n_fft, s, &A.tw);
+  int rc = dft_args(n_fft, s, &A);
   if (rc != TOMATIS_OK) return rc;
   const dim3 g((unsigned)((F + 1) / 2));
-#define AN_BAND(NN) \
-  if (n_fft == NN) hipLaunchKernelGGL((k_an_band_pair<NN>), g, dim3(kT), 0, s, A);
-  AN_BAND(256) AN_BAND(512) AN_BAND(1024) AN_BAND(2048) AN_BAND(4096) AN_BAND(8192)
-#undef AN_BAND
-  return an_launch();
+  return dispatch_m(A, [&](auto m, auto b) {
+    hipLaunchKernelGGL((k_an_band_pair<decltype(m)::value, decltype(b)::value>), g, dim3(kT), 0,
+                       s, A);
+  });
 }
 
 int tomatis_cal_gate_grid(const float* levels, int32_t n_fit, const int64_t* starts,

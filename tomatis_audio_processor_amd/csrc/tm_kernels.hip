@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "tm_common.h"
+#include "tm_host_dsp.h"
 #include "tm_fft.h"
 #include "tm_shared.h"
 #include "../../include/tomatis_hip.h"
@@ -1455,41 +1456,6 @@ static bool gate_exclusive(const TomatisStream& S) {
 }
 
 // in-place iterative radix-2 FFT in double (plan set-up: Bluestein filter)
-static void fft_host(std::vector<std::complex<double>>& a) {
-  const size_t n = a.size();
-  for (size_t i = 1, j = 0; i < n; ++i) {
-    size_t bit = n >> 1;
-    for (; j & bit; bit >>= 1) j ^= bit;
-    j ^= bit;
-    if (i < j) std::swap(a[i], a[j]);
-  }
-  for (size_t len = 2; len <= n; len <<= 1) {
-    for (size_t i = 0; i < n; i += len)
-      for (size_t k = 0; k < len / 2; ++k) {
-        const std::complex<double> w = std::polar(1.0, -2.0 * M_PI * (double)k / (double)len);
-        const std::complex<double> u = a[i + k], v = a[i + k + len / 2] * w;
-        a[i + k] = u + v;
-        a[i + k + len / 2] = u - v;
-      }
-  }
-}
-
-// numpy pairwise_sum's tree over n elements at offset off (loops_utils.h.src:
-// blocks of <= 128, split at n/2 rounded down to a multiple of 8): leaves in
-// order, and the postfix combination program (n <= 8192: one inner-loop call)
-static void pw_build(int off, int n, std::vector<int2>& lv, std::vector<int16_t>& prog) {
-  if (n <= 128) {
-    prog.push_back((int16_t)lv.size());
-    lv.push_back(make_int2(off, n));
-    return;
-  }
-  int n2 = n / 2;
-  n2 -= n2 % 8;
-  pw_build(off, n2, lv, prog);
-  pw_build(off + n2, n - n2, lv, prog);
-  prog.push_back(-1);
-}
-
 static int plan_build(tomatis_plan_s* p, const float* window) {
   const TomatisPlanDesc& d = p->d;
   const int N = d.n_fft, hop = d.hop, P = p->P;
@@ -1612,12 +1578,7 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
     if (p->lvl_any || N > cap64) {
       std::vector<int2> lv;
       std::vector<int16_t> prog;
-      // numpy's reduction hands the pairwise sum at most NPY_BUFSIZE = 8192
-      // elements per inner-loop call and adds the calls' results in order
-      for (int c0 = 0; c0 < N; c0 += 8192) {
-        pw_build(c0, std::min(8192, N - c0), lv, prog);
-        if (c0 > 0) prog.push_back(-1);
-      }
+      thost::pw_program(N, lv, prog);
       if ((int)lv.size() > kPwMaxLeaves) return TOMATIS_E_UNSUPPORTED;
       p->n_pw_leaf = (int)lv.size();
       p->n_pw_prog = (int)prog.size();
@@ -1747,19 +1708,8 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
       }
       if ((rc = dalloc_copy(&p->twL, tl))) return rc;
       if (p->blue) {
-        // chirp b_n = exp(i pi n^2 / N): n^2 mod 2N exact in integers
-        std::vector<std::complex<double>> bd(N), h(M, 0.0);
-        std::vector<float2> bf(N), hf(M);
-        for (int n = 0; n < N; ++n) {
-          const int64_t q = ((int64_t)n * n) % (2 * (int64_t)N);
-          bd[n] = std::polar(1.0, M_PI * (double)q / (double)N);
-          bf[n] = make_float2((float)bd[n].real(), (float)bd[n].imag());
-        }
-        for (int n = 0; n < N; ++n) h[n] = bd[n];
-        for (int n = 1; n < N; ++n) h[M - n] = bd[n];
-        fft_host(h);
-        for (int k = 0; k < M; ++k)
-          hf[k] = make_float2((float)(h[k].real() / M), (float)(h[k].imag() / M));
+        std::vector<float2> bf, hf;
+        thost::bluestein_tables(N, M, bf, hf);
         if ((rc = dalloc_copy(&p->blue_b, bf))) return rc;
         if ((rc = dalloc_copy(&p->blue_h, hf))) return rc;
       }

@@ -2,6 +2,8 @@
 // order in and out), Stockham autosort: one radix-2 stage when log2 N is odd,
 // then radix-4 stages; THREADS threads of the workgroup cooperate, barriers
 // between stages.  Twiddles tw[t] = exp(-2 pi i t / N) (float2, any memory).
+// lds_dft<M, BLUE>: DFT of any length n in LDS — M = n (power of two) or
+// Bluestein's chirp-z over M = 2^k >= 2n - 1 (tables from tm_host_dsp.h).
 // Used by the analysis spectra (tm_analysis.hip) and the any-size STFT path
 // of the transform unit (tm_transform.hip).
 #pragma once
@@ -87,5 +89,32 @@ __device__ __forceinline__ void lds_fft(float2* __restrict__ buf, const float2* 
   }
 }
 
+__device__ __forceinline__ float2 conjf2(float2 a) { return make_float2(a.x, -a.y); }
+__device__ __forceinline__ float2 cmul_conj(float2 a, float2 b) {  // a * conj(b)
+  return make_float2(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
+}
+
+// Forward DFT of buf[0, n) in LDS, in place; callers synchronise before.
+// BLUE: X[k] = conj(b_k) * IFFT_M(FFT_M(z * conj(b)) * H)[k] with
+// b_n = exp(i pi n^2 / n) and H = FFT_M(h) / M (h = b on [0, n), mirrored at
+// the top of [0, M)); the inverse FFT is conj(FFT(conj(.))).  buf holds M.
+template <int M, bool BLUE, int kT = 256>
+__device__ __forceinline__ void lds_dft(float2* buf, int n, const float2* __restrict__ tw,
+                                        const float2* __restrict__ bb,
+                                        const float2* __restrict__ bh) {
+  if constexpr (!BLUE) {
+    lds_fft<M, kT>(buf, tw);
+  } else {
+    for (int i = threadIdx.x; i < M; i += kT)
+      buf[i] = i < n ? cmul_conj(buf[i], bb[i]) : make_float2(0.f, 0.f);
+    __syncthreads();
+    lds_fft<M, kT>(buf, tw);
+    for (int k = threadIdx.x; k < M; k += kT) buf[k] = conjf2(cmul(buf[k], bh[k]));
+    __syncthreads();
+    lds_fft<M, kT>(buf, tw);
+    for (int k = threadIdx.x; k < n; k += kT) buf[k] = conjf2(cmul(buf[k], bb[k]));
+    __syncthreads();
+  }
+}
 
 }  // namespace tlds

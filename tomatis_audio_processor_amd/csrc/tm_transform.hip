@@ -753,30 +753,13 @@ __device__ __forceinline__ int stream_of_frame(const TomatisStream* st, int n, i
   return lo;
 }
 
-__device__ __forceinline__ float2 conjf2(float2 a) { return make_float2(a.x, -a.y); }
-__device__ __forceinline__ float2 cmul_conj(float2 a, float2 b) {  // a * conj(b)
-  return make_float2(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
-}
+using tlds::conjf2;
+using tlds::cmul_conj;
 
 // forward DFT of buf[0, N) in LDS, in place (callers synchronise before)
 template <int M, bool BLUE>
 __device__ __forceinline__ void lds_dft(float2* buf, const LdsArgs& A) {
-  if constexpr (!BLUE) {
-    tlds::lds_fft<M>(buf, A.tw);
-  } else {
-    const int N = A.n_fft;
-    for (int n = threadIdx.x; n < M; n += blockDim.x)
-      buf[n] = n < N ? cmul_conj(buf[n], A.blue_b[n]) : make_float2(0.f, 0.f);
-    __syncthreads();
-    tlds::lds_fft<M>(buf, A.tw);
-    for (int k = threadIdx.x; k < M; k += blockDim.x)
-      buf[k] = conjf2(tlds::cmul(buf[k], A.blue_h[k]));
-    __syncthreads();
-    tlds::lds_fft<M>(buf, A.tw);
-    for (int k = threadIdx.x; k < N; k += blockDim.x)
-      buf[k] = conjf2(tlds::cmul(buf[k], A.blue_b[k]));
-    __syncthreads();
-  }
+  tlds::lds_dft<M, BLUE>(buf, A.n_fft, A.tw, A.blue_b, A.blue_h);
 }
 
 // radix-2 Stockham over HBM buffers a -> b -> a ...; returns the buffer holding

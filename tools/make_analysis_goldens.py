@@ -11,7 +11,8 @@ Build-container only.  The modules import ``soundfile`` at top level (absent
 here): ``tools/_sf_stub`` satisfies the import; none of these functions touch
 files.  Fixtures hold only parameters and the reference's outputs.
 
-Usage:  MPLBACKEND=Agg python tools/make_analysis_goldens.py
+Usage:  MPLBACKEND=Agg python tools/make_analysis_goldens.py [--missing]
+(--missing: only cases without a fixture, leaving committed ones untouched)
 """
 from __future__ import annotations
 
@@ -38,7 +39,11 @@ def ref(mod):
 
 
 def main():
+    missing = "--missing" in sys.argv[1:]
     for c in AN_CASES:
+        p = os.path.join(REPO, "tests", "golden", c["name"] + ".npz")
+        if missing and os.path.exists(p):
+            continue
         x, y, states = an_inputs(c)
         out = {"meta": np.array(json.dumps(c))}
         if c["fn"] == "stft_mag_avg":
@@ -55,7 +60,6 @@ def main():
             freqs, c1, c2, n1, n2 = m.compute_conditional_spectrum(
                 x, y, c["sr"], states, c["n_fft"], c["hop"], c["level_threshold"])
             out.update(freqs=freqs, c1_db=c1, c2_db=c2, n1=np.array(n1), n2=np.array(n2))
-        p = os.path.join(REPO, "tests", "golden", c["name"] + ".npz")
         np.savez_compressed(p, **out)
         print(c["name"], {k: (v.shape, v.dtype) for k, v in out.items() if k != "meta"},
               {k: int(v) for k, v in out.items() if k in ("used", "n1", "n2")})
