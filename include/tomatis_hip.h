@@ -266,9 +266,16 @@ int tomatis_plan_error_bits(tomatis_plan_t plan, uint32_t* bits, int32_t reset,
  *       kernel where eligible, or always the separate tomatis_apply_limiter.
  *   TOMATIS_OPT_LIMITER_SPIN: polls a fused-limiter wave makes before it gives
  *       up (default 2^18; 0 forces TOMATIS_ERR_LIMITER_WAIT: fault-injection
- *       tests of the host's recovery path). */
+ *       tests of the host's recovery path).
+ *   TOMATIS_OPT_MINHOLD_SERIAL (0 default / 1): how tomatis_minhold_bisect runs
+ *       the bisection (same result bit for bit).  0: three steps per launch as
+ *       the 7 midpoints of their tree, 7 workgroups per stream over the chip,
+ *       when every stream's tables fit the LDS (else serial); 1: the 30 steps
+ *       in one workgroup per stream -- the small footprint to prefer when the
+ *       call overlaps another stream group's transform. */
 #define TOMATIS_OPT_FUSE_LIMITER 1
 #define TOMATIS_OPT_LIMITER_SPIN 2
+#define TOMATIS_OPT_MINHOLD_SERIAL 3
 int tomatis_plan_set_option(tomatis_plan_t plan, int32_t option, int64_t value);
 
 /* max |x| over n floats as float bits (out zeroed by caller). */

@@ -46,7 +46,8 @@ def test_header_constants_match_binding():
                       ("TOMATIS_ERR_LIMITER_WAIT", _lib.ERR_LIMITER_WAIT),
                       ("TOMATIS_ERR_PAIR_BARRIER", _lib.ERR_PAIR_BARRIER),
                       ("TOMATIS_OPT_FUSE_LIMITER", _lib.OPT_FUSE_LIMITER),
-                      ("TOMATIS_OPT_LIMITER_SPIN", _lib.OPT_LIMITER_SPIN)]:
+                      ("TOMATIS_OPT_LIMITER_SPIN", _lib.OPT_LIMITER_SPIN),
+                      ("TOMATIS_OPT_MINHOLD_SERIAL", _lib.OPT_MINHOLD_SERIAL)]:
         assert int(defs[name]) == val, name
 
 

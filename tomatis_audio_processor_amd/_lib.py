@@ -21,6 +21,7 @@ ERR_LIMITER_WAIT = 1     # TOMATIS_ERR_LIMITER_WAIT
 ERR_PAIR_BARRIER = 2     # TOMATIS_ERR_PAIR_BARRIER
 OPT_FUSE_LIMITER = 1     # TOMATIS_OPT_FUSE_LIMITER
 OPT_LIMITER_SPIN = 2     # TOMATIS_OPT_LIMITER_SPIN
+OPT_MINHOLD_SERIAL = 3   # TOMATIS_OPT_MINHOLD_SERIAL
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 F32, F64 = 0, 1

@@ -379,7 +379,7 @@ __global__ __launch_bounds__(kT) void k_an_spec_pair(SpecArgs A) {
   __shared__ float2 buf[M];
   const int f0 = blockIdx.x * 2, f1 = f0 + 1;
   const bool has1 = f1 < A.n_frames;
-  const int n = A.n_fft;
+  const int n = BLUE ? A.n_fft : M;  // constant for powers of two
   const int64_t p0 = (int64_t)f0 * A.hop, p1 = (int64_t)f1 * A.hop;
   for (int i = threadIdx.x; i < n; i += kT) {
     const float w = A.win[i];
@@ -416,7 +416,7 @@ __global__ __launch_bounds__(kT) void k_an_spec_pair(SpecArgs A) {
 template <int M, bool BLUE>
 __global__ __launch_bounds__(kT) void k_an_band_pair(SpecArgs A) {
   __shared__ float2 buf[M];
-  const int N = A.n_fft;
+  const int N = BLUE ? A.n_fft : M;
   __shared__ float red[kT / 64][4];
   const int f0 = blockIdx.x * 2, f1 = f0 + 1;
   const bool has1 = f1 < A.n_frames;
@@ -512,7 +512,7 @@ __global__ __launch_bounds__(kT) void k_an_spec_ratio(SpecArgs A) {
   __shared__ float2 buf[M];
   constexpr int kMaxUB = (M / 2 + 1 + kT - 1) / kT;  // bins per thread (n/2+1 <= M/2+1)
   const int f = blockIdx.x;
-  const int n = A.n_fft;
+  const int n = BLUE ? A.n_fft : M;  // constant for powers of two
   const int64_t p0 = (int64_t)f * A.hop;
   float ax[kMaxUB], ay[kMaxUB];
 #pragma unroll

@@ -835,6 +835,21 @@ __device__ void mh_simulate(const uint32_t* sym, int64_t F, int64_t seg, int mh,
 constexpr double kValidLevel = -70.0;
 constexpr int kSelRanks = 6;
 
+// h[d] += 1 for every lane with pred, the wave's equal digits merged into one
+// LDS atomic each (up to 4 distinct digits; the rest add per lane)
+__device__ __forceinline__ void wave_hist_add(uint32_t* h, uint32_t d, bool pred, int lane) {
+  uint64_t todo = __ballot(pred);
+  for (int it = 0; it < 4 && todo; ++it) {
+    const int leader = __ffsll((long long)todo) - 1;
+    const uint32_t ld = (uint32_t)__shfl((int)d, leader, 64);
+    const uint64_t same = __ballot(pred && d == ld) & todo;
+    if (lane == leader) atomicAdd(&h[ld], (uint32_t)__popcll(same));
+    todo &= ~same;
+    if ((same >> lane) & 1ull) pred = false;
+  }
+  if (pred) atomicAdd(&h[d], 1u);
+}
+
 __device__ __forceinline__ uint64_t f64_key(double v) {
   const uint64_t u = (uint64_t)__double_as_longlong(v);
   return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
@@ -899,22 +914,36 @@ __global__ __launch_bounds__(1024) void k_level_stats(const double* __restrict__
     const uint64_t hmask = pass ? (~0ull << (shift + 8)) : 0ull;
     for (int i = tid; i < kSelRanks * 256; i += blockDim.x) (&hist[0][0])[i] = 0;
     __syncthreads();
+    // ranks whose prefixes agree share one histogram (cls: the first such
+    // rank); levels cluster, so the adds are aggregated per wave and digit
     uint64_t pr[kSelRanks];
-    for (int r = 0; r < kSelRanks; ++r) pr[r] = pre[r];
-    for (int64_t i = tid; i < F; i += blockDim.x) {
-      const double v = lv[i];
-      if (!all && !(v > kValidLevel)) continue;
+    int cls[kSelRanks];
+#pragma unroll
+    for (int r = 0; r < kSelRanks; ++r) {
+      pr[r] = pre[r];
+      cls[r] = r;
+      for (int r2 = r - 1; r2 >= 0; --r2)
+        if (pr[r2] == pr[r]) cls[r] = r2;
+    }
+    for (int64_t i0 = 0; i0 < F; i0 += blockDim.x) {  // wave-uniform trip count
+      const int64_t i = i0 + tid;
+      const double v = i < F ? lv[i] : 0.0;
+      const bool ok = i < F && (all || v > kValidLevel);
       const uint64_t k = f64_key(v);
       const uint32_t d = (uint32_t)(k >> shift) & 255u;
 #pragma unroll
       for (int r = 0; r < kSelRanks; ++r)
-        if ((k & hmask) == pr[r]) atomicAdd(&hist[r][d], 1u);
+        if (cls[r] == r) wave_hist_add(hist[r], d, ok && (k & hmask) == pr[r], lane);
     }
     __syncthreads();
     if (wv < kSelRanks) {   // wave r resolves rank r's digit
       const int r = wv;
-      const uint32_t b0 = hist[r][4 * lane], b1 = hist[r][4 * lane + 1],
-                     b2 = hist[r][4 * lane + 2], b3 = hist[r][4 * lane + 3];
+      int cr = 0;
+#pragma unroll
+      for (int j = 0; j < kSelRanks; ++j)
+        if (j == r) cr = cls[j];
+      const uint32_t b0 = hist[cr][4 * lane], b1 = hist[cr][4 * lane + 1],
+                     b2 = hist[cr][4 * lane + 2], b3 = hist[cr][4 * lane + 3];
       const uint32_t tot = b0 + b1 + b2 + b3;
       uint32_t incl = tot;
       for (int o = 1; o < 64; o <<= 1) {
@@ -960,6 +989,122 @@ __global__ __launch_bounds__(1024) void k_level_stats(const double* __restrict__
   }
 }
 
+// ---------------------------------------------------------------------------
+// Speculative bisection (process_tomatis_adaptive.py:133-154, find_optimal_
+// threshold): the reference's 30-step bisection is sequential, one threshold
+// per step, and k_minhold runs it on one CU per stream.  k_mh_probe instead
+// evaluates the next THREE steps at once: the 7 midpoints of the depth-3 tree
+// of possible (t_low, t_high) paths, one workgroup each, computed by the same
+// (lo + hi) / 2 operations the sequential loop would apply along each path.
+// The last workgroup of a stream to finish (agent-scope arrival counter)
+// walks the taken path with the reference's best-diff, early-exit (diff <
+// 0.01) and branch rules, so the result is the sequential bisection's, bit
+// for bit, in 10 launches of 7 x n_streams workgroups instead of 30 steps on
+// n_streams CUs.  k_minhold then finishes states / alpha from best_T.
+// Streams whose tables spill to the HBM workspace keep the sequential kernel.
+// ---------------------------------------------------------------------------
+struct MhBisect {
+  double lo, hi, best_T, best_diff;
+  int32_t it, done, arrive, pad;
+};
+constexpr int kMhProbes = 7;
+
+__global__ void k_mh_init(const TomatisStream* __restrict__ st, int n_streams,
+                          const double* __restrict__ tlh, MhBisect* __restrict__ bs) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_streams) return;
+  const double lo = tlh[3 * s + 0], hi = tlh[3 * s + 1];
+  MhBisect B;
+  B.lo = lo;
+  B.hi = hi;
+  B.best_T = tlh[3 * s + 2];
+  B.best_diff = 1.0;
+  B.it = 0;
+  B.done = (st[s].n_frames > 0 && !(lo != lo)) ? 0 : 1;
+  B.arrive = 0;
+  B.pad = 0;
+  bs[s] = B;
+}
+
+__global__ __launch_bounds__(1024) void k_mh_probe(const double* __restrict__ levels,
+                                                   const TomatisStream* __restrict__ st,
+                                                   double target, double hyst, int mh,
+                                                   MhBisect* __restrict__ bs,
+                                                   int32_t* __restrict__ counts) {
+  const int s = blockIdx.x, j = blockIdx.y;
+  const MhBisect B = bs[s];  // written by the previous launch
+  if (B.done) return;        // uniform over the stream's workgroups
+  const TomatisStream S = st[s];
+  const int64_t F = S.n_frames;
+  const double* lv = levels + S.frame_base;
+  const int ns = 2 * (mh + 1);
+  const int64_t seg = mh_seg_len(F, ns);
+  const int nseg = (int)((F + seg - 1) / seg);
+  __shared__ uint16_t tf[kMhLdsTf];
+  __shared__ int32_t cnt[kMhLdsTf];
+  __shared__ uint32_t sym[kMhLdsSym];
+  // node j (BFS order; child 2n+1: c2 < target, so t_high = mid; 2n+2: t_low = mid)
+  const int depth = j == 0 ? 0 : (j < 3 ? 1 : 2);
+  int path[2];
+  for (int n = j, d = depth; d > 0; --d) {
+    path[d - 1] = n;
+    n = (n - 1) / 2;
+  }
+  double lo = B.lo, hi = B.hi;
+  for (int d = 0; d < depth; ++d) {
+    const double mid = (lo + hi) / 2;
+    if (path[d] & 1) hi = mid;
+    else lo = mid;
+  }
+  const double t_mid = (lo + hi) / 2;
+  const double ton = t_mid + hyst / 2, toff = t_mid - hyst / 2;
+  mh_symbols(lv, F, ton, toff, sym);
+  __syncthreads();
+  mh_simulate(sym, F, seg, mh, tf, cnt);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int id = mh, c = 0;  // start state: C1, since = mh
+    for (int g = 0; g < nseg; ++g) {
+      c += cnt[(int64_t)g * ns + id];
+      id = tf[(int64_t)g * ns + id];
+    }
+    __hip_atomic_store(counts + (int64_t)s * kMhProbes + j, c, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    const int old = __hip_atomic_fetch_add(&bs[s].arrive, 1, __ATOMIC_ACQ_REL,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    if (old == kMhProbes - 1) {  // last of the stream's probes: walk the taken path
+      MhBisect R = B;
+      int node = 0;
+      for (int d = 0; d < 3; ++d) {
+        const double mid = (R.lo + R.hi) / 2;
+        const int cn = __hip_atomic_load(counts + (int64_t)s * kMhProbes + node,
+                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const double c2 = (double)cn / (double)F;
+        const double diff = fabs(c2 - target);
+        if (diff < R.best_diff) {
+          R.best_diff = diff;
+          R.best_T = mid;
+        }
+        ++R.it;
+        if (diff < 0.01) {
+          R.done = 1;
+          break;
+        }
+        if (c2 < target) {
+          R.hi = mid;
+          node = 2 * node + 1;
+        } else {
+          R.lo = mid;
+          node = 2 * node + 2;
+        }
+      }
+      if (R.it >= 30) R.done = 1;
+      R.arrive = 0;
+      bs[s] = R;  // read by the next launch
+    }
+  }
+}
+
 __global__ __launch_bounds__(1024) void k_minhold(const double* __restrict__ levels,
                                                   const TomatisStream* __restrict__ st,
                                                   const double* __restrict__ tlh,
@@ -972,7 +1117,8 @@ __global__ __launch_bounds__(1024) void k_minhold(const double* __restrict__ lev
                                                   double* __restrict__ t_out,
                                                   uint8_t* __restrict__ states,
                                                   uint16_t* __restrict__ rows,
-                                                  double* __restrict__ alpha) {
+                                                  double* __restrict__ alpha,
+                                                  const MhBisect* __restrict__ bisected) {
   const int s = blockIdx.x;
   const TomatisStream S = st[s];
   const int64_t F = S.n_frames;
@@ -994,7 +1140,9 @@ __global__ __launch_bounds__(1024) void k_minhold(const double* __restrict__ lev
   double t_low = tlh[3 * s + 0], t_high = tlh[3 * s + 1];
   double best_T = tlh[3 * s + 2], best_diff = 1.0;
   const bool have_valid = !(t_low != t_low);
-  if (F > 0 && have_valid) {
+  if (bisected) {
+    best_T = bisected[s].best_T;  // k_mh_probe rounds did the bisection
+  } else if (F > 0 && have_valid) {
     for (int it = 0; it < 30; ++it) {
       const double t_mid = (t_low + t_high) / 2;
       const double ton = t_mid + hyst / 2, toff = t_mid - hyst / 2;
@@ -1044,6 +1192,9 @@ __global__ __launch_bounds__(1024) void k_minhold(const double* __restrict__ lev
     }
   }
   __syncthreads();
+  // the states also go to LDS (the transfer counts are no longer needed) so the
+  // alpha passes below read them without HBM round trips
+  uint8_t* st_l = (F <= (int64_t)sizeof(cnt_l)) ? reinterpret_cast<uint8_t*>(cnt_l) : nullptr;
   for (int g = threadIdx.x; g < nseg; g += blockDim.x) {
     const int id0 = seg_start[g];
     MhState stt{id0 > mh ? 1 : 0, id0 > mh ? id0 - (mh + 1) : id0};
@@ -1055,7 +1206,9 @@ __global__ __launch_bounds__(1024) void k_minhold(const double* __restrict__ lev
       for (int j = 0; j < n; ++j) {
         int c = 0;
         mh_word(stt, w >> (2 * j), 1, mh, c);
-        states[S.frame_base + k + j] = stt.c2 ? 2 : 1;
+        const uint8_t v = stt.c2 ? 2 : 1;
+        states[S.frame_base + k + j] = v;
+        if (st_l) st_l[k + j] = v;
       }
     }
   }
@@ -1069,7 +1222,7 @@ __global__ __launch_bounds__(1024) void k_minhold(const double* __restrict__ lev
     const double step = xf > 0 ? 1.0 / xf : 1.0;
     const int xfe = xf > 0 ? xf : 1;
     const int J = xf + 2;
-    const uint8_t* stt = states + S.frame_base;
+    const uint8_t* stt = st_l ? st_l : states + S.frame_base;
     const int64_t CHK = max<int64_t>(256, (F + kMhAlphaChunks - 1) / kMhAlphaChunks);
     const int nch = (int)((F + CHK - 1) / CHK);
     __shared__ int32_t a_q[kMhAlphaChunks];
@@ -1333,6 +1486,9 @@ struct tomatis_plan_s {
   int64_t* mh_off = nullptr;
   uint32_t* mh_sym = nullptr;
   int64_t* mh_soff = nullptr;
+  MhBisect* mh_bs = nullptr;  // speculative bisection state per stream
+  int mh_serial = 0;          // TOMATIS_OPT_MINHOLD_SERIAL
+  int32_t* mh_pc = nullptr;   // probe counts [stream][kMhProbes]
   float* gperm = nullptr;
   int gperm_rows = 0;
   // fused limiter
@@ -1424,7 +1580,7 @@ int tomatis_plan_destroy(tomatis_plan_t p) {
   if (!p) return TOMATIS_OK;
   void* ptrs[] = {p->st, p->runs, p->lblocks, p->segs, p->seg_first, p->seg_count, p->tf,
                   p->seg_start, p->win, p->winS, p->win2, p->winv, p->twN, p->twP, p->scratch,
-                  p->pos_base, p->chunks, p->mh_tf, p->mh_cnt, p->mh_off, p->mh_sym, p->mh_soff, p->gperm,
+                  p->pos_base, p->chunks, p->mh_tf, p->mh_cnt, p->mh_off, p->mh_sym, p->mh_soff, p->mh_bs, p->mh_pc, p->gperm,
                   p->grp_base, p->leaf_base, p->leaves, p->gsum, p->gcarry, p->gcarry_in,
                   p->aq, p->afin, p->acin,
                   p->chunk_need, p->chunk_done, p->chunk_rng, p->err, p->twL,
@@ -1829,6 +1985,11 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
     if (soff[ns] > 0 &&
         hipMalloc(reinterpret_cast<void**>(&p->mh_sym), soff[ns] * sizeof(uint32_t)))
       return TOMATIS_E_NOMEM;
+    if (ns > 0) {
+      if (hipMalloc(reinterpret_cast<void**>(&p->mh_bs), ns * sizeof(MhBisect))) return TOMATIS_E_NOMEM;
+      if (hipMalloc(reinterpret_cast<void**>(&p->mh_pc), ns * kMhProbes * sizeof(int32_t)))
+        return TOMATIS_E_NOMEM;
+    }
   }
   return TOMATIS_OK;
 }
@@ -2148,9 +2309,21 @@ int tomatis_minhold_bisect(tomatis_plan_t p, const double* levels, const double*
   if (!p || !levels || !tlh || !states) return TOMATIS_E_ARG;
   if (p->n_streams == 0) return TOMATIS_OK;
   hipStream_t s = (hipStream_t)hs;
+  // speculative rounds when every stream's tables fit the probe kernel's LDS
+  // (no HBM workspace); TOMATIS_MH_SERIAL keeps the one-CU-per-stream loop
+  const bool spec = !p->mh_serial && p->mh_bs && !p->mh_tf && !p->mh_sym;
+  if (spec) {
+    const int ns = p->n_streams;
+    hipLaunchKernelGGL(k_mh_init, dim3((ns + 255) / 256), dim3(256), 0, s, p->st, ns, tlh,
+                       p->mh_bs);
+    for (int r = 0; r < 10; ++r)  // 30 bisection steps, three per launch
+      hipLaunchKernelGGL(k_mh_probe, dim3(ns, kMhProbes), dim3(1024), 0, s, levels, p->st,
+                         target_c2, hyst_db, p->d.min_hold_frames, p->mh_bs, p->mh_pc);
+  }
   hipLaunchKernelGGL(k_minhold, dim3(p->n_streams), dim3(1024), 0, s, levels, p->st, tlh,
                      target_c2, hyst_db, p->d.min_hold_frames, p->d.xfade_frames, 1, p->mh_tf,
-                     p->mh_cnt, p->mh_off, p->mh_sym, p->mh_soff, t_out, states, rows, alpha_out);
+                     p->mh_cnt, p->mh_off, p->mh_sym, p->mh_soff, t_out, states, rows, alpha_out,
+                     spec ? p->mh_bs : nullptr);
   return launch_check();
 }
 
@@ -2365,6 +2538,7 @@ int tomatis_plan_set_option(tomatis_plan_t p, int32_t option, int64_t value) {
       if (value < 0 || value > (1 << 24)) return TOMATIS_E_ARG;
       p->lim_spin = (int)value;
       return TOMATIS_OK;
+    case TOMATIS_OPT_MINHOLD_SERIAL: p->mh_serial = value != 0; return TOMATIS_OK;
     default: return TOMATIS_E_ARG;
   }
 }

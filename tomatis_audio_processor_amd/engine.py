@@ -17,6 +17,7 @@ Reference behaviour reproduced per mode (file:line):
 from __future__ import annotations
 
 import ctypes as C
+import os
 import time
 import warnings
 from dataclasses import dataclass, field
@@ -26,7 +27,7 @@ import numpy as np
 
 from . import dsp
 from ._lib import (ERR_LIMITER_WAIT, ERR_PAIR_BARRIER, F32, F64, NORM_EPS, NORM_MAX,
-                   OPT_FUSE_LIMITER, OPT_LIMITER_SPIN, TomatisPlanDesc, TomatisStream, check, lib,
+                   OPT_FUSE_LIMITER, OPT_LIMITER_SPIN, OPT_MINHOLD_SERIAL, TomatisPlanDesc, TomatisStream, check, lib,
                    ptr, stream_handle)
 
 PEAK_LIMIT = 0.999
@@ -200,21 +201,24 @@ def _host_pool():
     return _POOL
 
 
-def _levels_threaded(r: np.ndarray, out: np.ndarray):
+def _levels_threaded(r: np.ndarray, out: np.ndarray, tmp: np.ndarray = None):
     """``dsp.r_to_level(r)`` into ``out``: the same ufunc chain with in-place
-    temporaries (bit-identical: the same loops on the same dtypes), in slices on
-    the host pool when TOMATIS_LOG10_THREADS > 1 (numpy's SIMD log10 does not
-    scale over threads on the measured hosts, so one thread by default)."""
-    import os
+    temporaries (bit-identical: the same loops on the same dtypes; the last
+    multiply runs in r's dtype and casts into the float64 ``out`` in its inner
+    loop), in slices on the host pool when TOMATIS_LOG10_THREADS > 1 (numpy's
+    SIMD log10 does not scale over threads on the measured hosts, so one thread
+    by default).  ``tmp``: a reusable buffer of r's dtype (a fresh one per call
+    costs its page faults)."""
     n = len(r)
-    tmp = np.empty(n, np.asarray(r).dtype)
+    dt = np.asarray(r).dtype
+    if tmp is None or len(tmp) < n or tmp.dtype != dt:
+        tmp = np.empty(n, dt)
     k = int(os.environ.get("TOMATIS_LOG10_THREADS", "1"))
 
     def part(a, b):
         np.add(r[a:b], dsp.EPS, out=tmp[a:b])
         np.log10(tmp[a:b], out=tmp[a:b])
-        np.multiply(tmp[a:b], 20.0, out=tmp[a:b])
-        out[a:b] = tmp[a:b]
+        np.multiply(tmp[a:b], 20.0, out=out[a:b], dtype=dt, casting="unsafe")
 
     if k <= 1 or n < (1 << 16):
         part(0, n)
@@ -547,9 +551,11 @@ class AdaptivePipeline:
         self.peaks = torch.zeros(max(1, self.plan.total_chunks), dtype=torch.int32, device=dev)
         self.inpk = torch.zeros(max(1, ss.n_streams), dtype=torch.int32, device=dev)
         self._lv_pin = None   # page-locked staging of r and the host levels (allocated once)
+        self._lv_tmp = None   # host temporaries of the level chain (allocated once)
         self._pk_pin = torch.empty(max(1, ss.n_streams), dtype=torch.int32, pin_memory=True)
         self.stream = None    # torch stream the pipeline runs on (None: the current one)
         self.done = torch.cuda.Event()
+        self.prep_done = torch.cuda.Event()  # after the bisection / states launch
         self._tlh = torch.empty(3 * max(1, ss.n_streams), dtype=torch.float64, device=dev)
         self.gains = torch.from_numpy(np.stack(rows)).to(dev)
         self.n_rows = len(rows)
@@ -583,8 +589,8 @@ class AdaptivePipeline:
         """The pass as a generator that yields wherever the host would wait for
         the device (the input peaks, the frame r) and before the transform, so a
         driver can interleave several pipelines on their own streams
-        (AdaptiveGroups).  ``after``: a callable giving an event the transform
-        waits for (launch order)."""
+        (AdaptiveGroups).  ``after``: a callable giving an event (or a list of
+        events) the transform waits for."""
         torch = _torch()
         strm = self.stream or torch.cuda.current_stream()
         L, P = lib(), self.plan.h
@@ -625,6 +631,8 @@ class AdaptivePipeline:
         Ft = self.plan.total_frames
         if self._lv_pin is None:
             self._lv_pin = torch.empty(max(1, Ft), dtype=torch.float64, pin_memory=True)
+            self._lv32_pin = torch.empty(max(1, Ft), dtype=torch.float32, pin_memory=True)
+            self._lv32_dev = torch.empty(max(1, Ft), dtype=torch.float32, device=ss.x.device)
             self._r_pin = {F32: torch.empty(max(1, Ft), dtype=torch.float32, pin_memory=True),
                            F64: torch.empty(max(1, Ft), dtype=torch.float64, pin_memory=True)}
         with torch.cuda.stream(strm):
@@ -642,28 +650,50 @@ class AdaptivePipeline:
                     self._r_pin[pr][:Ft].copy_(rd[:Ft], non_blocking=True)
             ev.record()
         yield
-        ev.synchronize()
-        phase("r_d2h")
         # levels of every frame by the same elementwise numpy call as the
-        # reference's per-frame one, written into the page-locked upload block;
-        # per-stream order statistics (p5, p95, median of the valid levels) then
-        # on the device
-        lv = self._lv_pin.numpy()[:Ft]
-        rs = {pr: self._r_pin[pr].numpy()[:Ft] for pr in (F32, F64) if pr in prec}
-        if len(rs) == 1:
-            _levels_threaded(next(iter(rs.values())), lv)
-        else:
-            lv32 = np.empty(Ft, np.float64)
-            lv64 = np.empty(Ft, np.float64)
-            _levels_threaded(rs[F32], lv32)
-            _levels_threaded(rs[F64], lv64)
-            for i in range(ss.n_streams):
-                a, F = sts[i].frame_base, sts[i].n_frames
-                lv[a:a + F] = (lv32 if prec[i] == F32 else lv64)[a:a + F]
-        phase("log10")
+        # reference's per-frame one, written into a page-locked upload block (on
+        # a host thread, so several stream groups' chains overlap); per-stream
+        # order statistics (p5, p95, median of the valid levels) then on the
+        # device
+        if self._lv_tmp is None:
+            self._lv_tmp = {F32: np.empty(max(1, Ft), np.float32),
+                            F64: np.empty(max(1, Ft), np.float64)}
+
+        def host_levels():
+            ev.synchronize()
+            rs = {pr: self._r_pin[pr].numpy()[:Ft] for pr in (F32, F64) if pr in prec}
+            if set(rs) == {F32}:
+                # float32 levels (their float64 values are exact): the last
+                # multiply stays in float32, the device widens them
+                tmp = self._lv_tmp[F32][:Ft]
+                np.add(rs[F32], dsp.EPS, out=tmp)
+                np.log10(tmp, out=tmp)
+                np.multiply(tmp, 20.0, out=self._lv32_pin.numpy()[:Ft])
+                return F32
+            lv = self._lv_pin.numpy()[:Ft]
+            if len(rs) == 1:
+                _levels_threaded(rs[F64], lv, self._lv_tmp[F64])
+            else:
+                lv32 = np.empty(Ft, np.float64)
+                lv64 = np.empty(Ft, np.float64)
+                _levels_threaded(rs[F32], lv32, self._lv_tmp[F32])
+                _levels_threaded(rs[F64], lv64, self._lv_tmp[F64])
+                for i in range(ss.n_streams):
+                    a, F = sts[i].frame_base, sts[i].n_frames
+                    lv[a:a + F] = (lv32 if prec[i] == F32 else lv64)[a:a + F]
+            return F64
+
+        fut = _host_pool().submit(host_levels)
+        yield
+        up = fut.result()
+        phase("r_d2h+log10")
         with torch.cuda.stream(strm):
             hs = stream_handle()
-            self.levels[:Ft].copy_(self._lv_pin[:Ft], non_blocking=True)
+            if up == F32:
+                self._lv32_dev[:Ft].copy_(self._lv32_pin[:Ft], non_blocking=True)
+                self.levels[:Ft].copy_(self._lv32_dev[:Ft])
+            else:
+                self.levels[:Ft].copy_(self._lv_pin[:Ft], non_blocking=True)
             tl = self._tlh
             check(L.tomatis_level_stats(P, ptr(self.levels), ptr(tl), hs), "level_stats")
             phase("upload+stats")
@@ -672,12 +702,16 @@ class AdaptivePipeline:
                                            self.hyst_db, ptr(self.t_out), ptr(self.states),
                                            ptr(self.rows), ptr(self.alpha), hs), "minhold_bisect")
             phase("bisect+minhold")
+            self.prep_done.record()
         yield   # (a driver launches every group's statistics before the transforms)
         with torch.cuda.stream(strm):
             hs = stream_handle()
             # 4. STFT-gain-OLA, normalise, restore, global limiter
-            if after is not None and after() is not None:
-                strm.wait_event(after())
+            if after is not None:
+                evs = after()
+                for e in (evs if isinstance(evs, (list, tuple)) else [evs]):
+                    if e is not None:
+                        strm.wait_event(e)
             if marks and marks[0] is not None:
                 marks[0].record()
             self._transform()
@@ -761,10 +795,17 @@ class AdaptiveGroups:
                 cuts.append(i + 1)
         cuts.append(ss.n_streams)
         self.pipes = []
-        for a, b in zip(cuts[:-1], cuts[1:]):
+        # bisection: speculative over the chip while no transform runs; with
+        # TOMATIS_C3_SYNC=chain later groups' overlap the previous transform and
+        # take one CU per stream (TOMATIS_MH_MODE=spec / serial: all groups)
+        mh_mode = os.environ.get("TOMATIS_MH_MODE", "auto")
+        chain = os.environ.get("TOMATIS_C3_SYNC", "first") == "chain"
+        for g, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
             sub = StreamSet(x=ss.x, offs=ss.offs[a:b], lens=ss.lens[a:b], ch=ss.ch, sr=ss.sr)
             p = AdaptivePipeline(sub, out=(self.y, offs[a:b]), **params)
             p.stream = torch.cuda.Stream()
+            serial = mh_mode == "serial" or (mh_mode == "auto" and chain and g > 0)
+            p.plan.set_option(OPT_MINHOLD_SERIAL, int(serial))
             self.pipes.append(p)
         self.ss = ss
 
@@ -775,12 +816,23 @@ class AdaptiveGroups:
             p.stream.wait_stream(cur)
         G = len(self.pipes)
         gens = []
+        # transforms in group order; the first also waits for every group's
+        # statistics: a later group's small bisection / states kernels launched
+        # behind a running transform would wait for its workgroups to drain
+        # (measured: 5.8 ms for a 0.35 ms kernel) and delay the next transform
+        # (TOMATIS_C3_SYNC=chain: only the previous transform)
+        first_all = os.environ.get("TOMATIS_C3_SYNC", "first") != "chain"
         for g, p in enumerate(self.pipes):
             mk = None
             if marks:
                 mk = (marks[0] if g == 0 else None, marks[1] if g == G - 1 else None)
-            prev = self.pipes[g - 1] if g else None
-            gens.append(p.steps(mk, after=(lambda q=prev: q.done) if prev else None))
+            if g:
+                after = (lambda q=self.pipes[g - 1]: q.done)
+            elif first_all and G > 1:
+                after = (lambda: [q.prep_done for q in self.pipes[1:]])
+            else:
+                after = None
+            gens.append(p.steps(mk, after=after))
         live = list(gens)
         while live:
             for gen in list(live):
