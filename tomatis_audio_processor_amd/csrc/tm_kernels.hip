@@ -994,13 +994,14 @@ __global__ __launch_bounds__(1024) void k_level_stats(const double* __restrict__
 // threshold): the reference's 30-step bisection is sequential, one threshold
 // per step, and k_minhold runs it on one CU per stream.  k_mh_probe instead
 // evaluates the next THREE steps at once: the 7 midpoints of the depth-3 tree
-// of possible (t_low, t_high) paths, one workgroup each, computed by the same
+// of possible (t_low, t_high) paths, each over a few workgroups, computed by the same
 // (lo + hi) / 2 operations the sequential loop would apply along each path.
 // The last workgroup of a stream to finish (agent-scope arrival counter)
 // walks the taken path with the reference's best-diff, early-exit (diff <
 // 0.01) and branch rules, so the result is the sequential bisection's, bit
-// for bit, in 10 launches of 7 x n_streams workgroups instead of 30 steps on
-// n_streams CUs.  k_minhold then finishes states / alpha from best_T.
+// for bit, in 10 launches of 7 x parts x n_streams workgroups instead of 30
+// steps on n_streams CUs.  An 11th launch builds best_T's transfer tables the
+// same way; k_minhold then finishes states / alpha from them.
 // Streams whose tables spill to the HBM workspace keep the sequential kernel.
 // ---------------------------------------------------------------------------
 struct MhBisect {
@@ -1026,47 +1027,103 @@ __global__ void k_mh_init(const TomatisStream* __restrict__ st, int n_streams,
   bs[s] = B;
 }
 
+// One probe (or the final threshold) per (stream, slot) is split over `parts`
+// workgroups, each simulating a contiguous range of segments from every start
+// state into the slot's global tables; the last of them (agent-scope arrival
+// counter) stages the tables in LDS and runs the segment chain.  Slots 0-6:
+// the tree midpoints (then, per stream, the last probe walks the taken path);
+// slot 7: best_T, whose tables k_minhold consumes.
+constexpr int kMhSlots = kMhProbes + 1;
+
 __global__ __launch_bounds__(1024) void k_mh_probe(const double* __restrict__ levels,
                                                    const TomatisStream* __restrict__ st,
                                                    double target, double hyst, int mh,
                                                    MhBisect* __restrict__ bs,
-                                                   int32_t* __restrict__ counts) {
-  const int s = blockIdx.x, j = blockIdx.y;
+                                                   int32_t* __restrict__ counts,
+                                                   uint16_t* __restrict__ gtf,
+                                                   int32_t* __restrict__ gcnt,
+                                                   const int64_t* __restrict__ goff,
+                                                   int32_t* __restrict__ arrive, int final_T) {
+  const int s = blockIdx.x, j = final_T ? kMhProbes : blockIdx.y;
+  const int part = blockIdx.z, parts = gridDim.z;
   const MhBisect B = bs[s];  // written by the previous launch
-  if (B.done) return;        // uniform over the stream's workgroups
+  if (B.done && !final_T) return;  // uniform over the stream's workgroups
   const TomatisStream S = st[s];
   const int64_t F = S.n_frames;
+  if (F == 0) return;
   const double* lv = levels + S.frame_base;
   const int ns = 2 * (mh + 1);
   const int64_t seg = mh_seg_len(F, ns);
   const int nseg = (int)((F + seg - 1) / seg);
-  __shared__ uint16_t tf[kMhLdsTf];
-  __shared__ int32_t cnt[kMhLdsTf];
+  __shared__ uint16_t tf_l[kMhLdsTf];
+  __shared__ int32_t cnt_l[kMhLdsTf];
   __shared__ uint32_t sym[kMhLdsSym];
-  // node j (BFS order; child 2n+1: c2 < target, so t_high = mid; 2n+2: t_low = mid)
-  const int depth = j == 0 ? 0 : (j < 3 ? 1 : 2);
-  int path[2];
-  for (int n = j, d = depth; d > 0; --d) {
-    path[d - 1] = n;
-    n = (n - 1) / 2;
+  __shared__ int last;
+  double t_mid;
+  if (final_T) {
+    t_mid = B.best_T;
+  } else {
+    // node j (BFS order; child 2n+1: c2 < target, so t_high = mid; 2n+2: t_low = mid)
+    const int depth = j == 0 ? 0 : (j < 3 ? 1 : 2);
+    int path[2] = {0, 0};
+    for (int n = j, d = depth; d > 0; --d) {
+      path[d - 1] = n;
+      n = (n - 1) / 2;
+    }
+    double lo = B.lo, hi = B.hi;
+    for (int d = 0; d < depth; ++d) {
+      const double mid = (lo + hi) / 2;
+      if (path[d] & 1) hi = mid;
+      else lo = mid;
+    }
+    t_mid = (lo + hi) / 2;
   }
-  double lo = B.lo, hi = B.hi;
-  for (int d = 0; d < depth; ++d) {
-    const double mid = (lo + hi) / 2;
-    if (path[d] & 1) hi = mid;
-    else lo = mid;
-  }
-  const double t_mid = (lo + hi) / 2;
   const double ton = t_mid + hyst / 2, toff = t_mid - hyst / 2;
-  mh_symbols(lv, F, ton, toff, sym);
-  __syncthreads();
-  mh_simulate(sym, F, seg, mh, tf, cnt);
+  // this workgroup's segments [g0, g1): symbols of their frames, then every
+  // (segment, start state) walked into the slot's tables
+  const int g0 = (int)((int64_t)nseg * part / parts), g1 = (int)((int64_t)nseg * (part + 1) / parts);
+  uint16_t* tf = gtf + goff[s] + (int64_t)j * nseg * ns;
+  int32_t* cn = gcnt + goff[s] + (int64_t)j * nseg * ns;
+  if (g0 < g1) {
+    const int64_t k0 = (int64_t)g0 * seg, k1 = min<int64_t>((int64_t)g1 * seg, F);
+    mh_symbols(lv + k0, k1 - k0, ton, toff, sym);  // seg % 16 == 0: word-aligned
+    __syncthreads();
+    const int nwork = (g1 - g0) * ns;
+    for (int w = threadIdx.x; w < nwork; w += blockDim.x) {
+      const int sg = w / ns, s0 = w - sg * ns;
+      const int64_t a = (int64_t)sg * seg, b = min<int64_t>(a + seg, k1 - k0);
+      MhState q{s0 > mh ? 1 : 0, s0 > mh ? s0 - (mh + 1) : s0};
+      int c = 0;
+      for (int64_t k = a; k < b; k += 16) mh_word(q, sym[k >> 4], (int)min<int64_t>(16, b - k), mh, c);
+      const int64_t e = (int64_t)(g0 + sg) * ns + s0;
+      tf[e] = (uint16_t)(q.c2 * (mh + 1) + q.since);
+      cn[e] = c;
+    }
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
+    __threadfence();  // this workgroup's tables before its arrival
+    const int old = __hip_atomic_fetch_add(arrive + (int64_t)s * kMhSlots + j, 1, __ATOMIC_ACQ_REL,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    last = old == parts - 1;
+  }
+  __syncthreads();
+  if (!last || final_T) {
+    if (last && threadIdx.x == 0) arrive[(int64_t)s * kMhSlots + j] = 0;
+    return;  // the final tables are read by k_minhold (next launch)
+  }
+  __threadfence();
+  for (int e = threadIdx.x; e < nseg * ns; e += blockDim.x) {
+    tf_l[e] = __hip_atomic_load(tf + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    cnt_l[e] = __hip_atomic_load(cn + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    arrive[(int64_t)s * kMhSlots + j] = 0;
     int id = mh, c = 0;  // start state: C1, since = mh
     for (int g = 0; g < nseg; ++g) {
-      c += cnt[(int64_t)g * ns + id];
-      id = tf[(int64_t)g * ns + id];
+      c += cnt_l[g * ns + id];
+      id = tf_l[g * ns + id];
     }
     __hip_atomic_store(counts + (int64_t)s * kMhProbes + j, c, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
@@ -1077,9 +1134,9 @@ __global__ __launch_bounds__(1024) void k_mh_probe(const double* __restrict__ le
       int node = 0;
       for (int d = 0; d < 3; ++d) {
         const double mid = (R.lo + R.hi) / 2;
-        const int cn = __hip_atomic_load(counts + (int64_t)s * kMhProbes + node,
-                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const double c2 = (double)cn / (double)F;
+        const int cnv = __hip_atomic_load(counts + (int64_t)s * kMhProbes + node,
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const double c2 = (double)cnv / (double)F;
         const double diff = fabs(c2 - target);
         if (diff < R.best_diff) {
           R.best_diff = diff;
@@ -1118,7 +1175,10 @@ __global__ __launch_bounds__(1024) void k_minhold(const double* __restrict__ lev
                                                   uint8_t* __restrict__ states,
                                                   uint16_t* __restrict__ rows,
                                                   double* __restrict__ alpha,
-                                                  const MhBisect* __restrict__ bisected) {
+                                                  const MhBisect* __restrict__ bisected,
+                                                  const uint16_t* __restrict__ gtf,
+                                                  const int32_t* __restrict__ gcnt,
+                                                  const int64_t* __restrict__ goff) {
   const int s = blockIdx.x;
   const TomatisStream S = st[s];
   const int64_t F = S.n_frames;
@@ -1180,9 +1240,18 @@ __global__ __launch_bounds__(1024) void k_minhold(const double* __restrict__ lev
   // final states: segment transfer tables, sequential segment starts, then
   // every segment re-walked from its start writing states
   mh_symbols(lv, F, ton, toff, sym);
-  __syncthreads();
-  mh_simulate(sym, F, seg, mh, tf, cnt);
-  __syncthreads();
+  if (bisected) {  // tables of best_T from k_mh_probe's final slot: stage in LDS
+    const int64_t o = goff[s] + (int64_t)kMhProbes * nseg * ns;
+    for (int e = threadIdx.x; e < nseg * ns; e += blockDim.x) {
+      tf[e] = gtf[o + e];
+      cnt[e] = gcnt[o + e];
+    }
+    __syncthreads();
+  } else {
+    __syncthreads();
+    mh_simulate(sym, F, seg, mh, tf, cnt);
+    __syncthreads();
+  }
   __shared__ uint16_t seg_start[4096];
   if (threadIdx.x == 0) {
     int id = init_id;
@@ -1489,6 +1558,11 @@ struct tomatis_plan_s {
   MhBisect* mh_bs = nullptr;  // speculative bisection state per stream
   int mh_serial = 0;          // TOMATIS_OPT_MINHOLD_SERIAL
   int32_t* mh_pc = nullptr;   // probe counts [stream][kMhProbes]
+  uint16_t* mh_gtf = nullptr; // probe tables [stream][kMhSlots][nseg * ns]
+  int32_t* mh_gcnt = nullptr;
+  int64_t* mh_goff = nullptr;
+  int32_t* mh_arr = nullptr;  // probe arrival counters [stream][kMhSlots]
+  int mh_parts = 1;           // workgroups per probe
   float* gperm = nullptr;
   int gperm_rows = 0;
   // fused limiter
@@ -1580,7 +1654,7 @@ int tomatis_plan_destroy(tomatis_plan_t p) {
   if (!p) return TOMATIS_OK;
   void* ptrs[] = {p->st, p->runs, p->lblocks, p->segs, p->seg_first, p->seg_count, p->tf,
                   p->seg_start, p->win, p->winS, p->win2, p->winv, p->twN, p->twP, p->scratch,
-                  p->pos_base, p->chunks, p->mh_tf, p->mh_cnt, p->mh_off, p->mh_sym, p->mh_soff, p->mh_bs, p->mh_pc, p->gperm,
+                  p->pos_base, p->chunks, p->mh_tf, p->mh_cnt, p->mh_off, p->mh_sym, p->mh_soff, p->mh_bs, p->mh_pc, p->mh_gtf, p->mh_gcnt, p->mh_goff, p->mh_arr, p->gperm,
                   p->grp_base, p->leaf_base, p->leaves, p->gsum, p->gcarry, p->gcarry_in,
                   p->aq, p->afin, p->acin,
                   p->chunk_need, p->chunk_done, p->chunk_rng, p->err, p->twL,
@@ -1985,10 +2059,28 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
     if (soff[ns] > 0 &&
         hipMalloc(reinterpret_cast<void**>(&p->mh_sym), soff[ns] * sizeof(uint32_t)))
       return TOMATIS_E_NOMEM;
-    if (ns > 0) {
+    if (ns > 0 && off[ns] == 0 && soff[ns] == 0) {  // speculative path: tables fit
       if (hipMalloc(reinterpret_cast<void**>(&p->mh_bs), ns * sizeof(MhBisect))) return TOMATIS_E_NOMEM;
       if (hipMalloc(reinterpret_cast<void**>(&p->mh_pc), ns * kMhProbes * sizeof(int32_t)))
         return TOMATIS_E_NOMEM;
+      std::vector<int64_t> goff(ns + 1, 0);
+      int max_nseg = 1;
+      for (int s = 0; s < ns; ++s) {
+        const int64_t F = p->hs[s].n_frames;
+        const int64_t nseg = F > 0 ? (F + mh_seg_len(F, nsm) - 1) / mh_seg_len(F, nsm) : 0;
+        goff[s + 1] = goff[s] + kMhSlots * nseg * nsm;
+        max_nseg = std::max(max_nseg, (int)nseg);
+      }
+      // workgroups per probe: a few segments each (one pass of the block's
+      // threads over their (segment, start) pairs), at most 8
+      p->mh_parts = std::max(1, std::min(8, (max_nseg * nsm + 767) / 768));
+      if ((rc = dalloc_copy(&p->mh_goff, goff))) return rc;
+      if (goff[ns] > 0) {
+        if (hipMalloc(reinterpret_cast<void**>(&p->mh_gtf), goff[ns] * sizeof(uint16_t))) return TOMATIS_E_NOMEM;
+        if (hipMalloc(reinterpret_cast<void**>(&p->mh_gcnt), goff[ns] * sizeof(int32_t))) return TOMATIS_E_NOMEM;
+      }
+      if (hipMalloc(reinterpret_cast<void**>(&p->mh_arr), ns * kMhSlots * sizeof(int32_t))) return TOMATIS_E_NOMEM;
+      if (hipMemset(p->mh_arr, 0, ns * kMhSlots * sizeof(int32_t))) return TOMATIS_E_HIP;
     }
   }
   return TOMATIS_OK;
@@ -2311,19 +2403,23 @@ int tomatis_minhold_bisect(tomatis_plan_t p, const double* levels, const double*
   hipStream_t s = (hipStream_t)hs;
   // speculative rounds when every stream's tables fit the probe kernel's LDS
   // (no HBM workspace); TOMATIS_MH_SERIAL keeps the one-CU-per-stream loop
-  const bool spec = !p->mh_serial && p->mh_bs && !p->mh_tf && !p->mh_sym;
+  const bool spec = !p->mh_serial && p->mh_bs && p->mh_gtf;
   if (spec) {
-    const int ns = p->n_streams;
+    const int ns = p->n_streams, P = p->mh_parts, mh = p->d.min_hold_frames;
     hipLaunchKernelGGL(k_mh_init, dim3((ns + 255) / 256), dim3(256), 0, s, p->st, ns, tlh,
                        p->mh_bs);
     for (int r = 0; r < 10; ++r)  // 30 bisection steps, three per launch
-      hipLaunchKernelGGL(k_mh_probe, dim3(ns, kMhProbes), dim3(1024), 0, s, levels, p->st,
-                         target_c2, hyst_db, p->d.min_hold_frames, p->mh_bs, p->mh_pc);
+      hipLaunchKernelGGL(k_mh_probe, dim3(ns, kMhProbes, P), dim3(1024), 0, s, levels, p->st,
+                         target_c2, hyst_db, mh, p->mh_bs, p->mh_pc, p->mh_gtf, p->mh_gcnt,
+                         p->mh_goff, p->mh_arr, 0);
+    hipLaunchKernelGGL(k_mh_probe, dim3(ns, 1, P), dim3(1024), 0, s, levels, p->st, target_c2,
+                       hyst_db, mh, p->mh_bs, p->mh_pc, p->mh_gtf, p->mh_gcnt, p->mh_goff,
+                       p->mh_arr, 1);
   }
   hipLaunchKernelGGL(k_minhold, dim3(p->n_streams), dim3(1024), 0, s, levels, p->st, tlh,
                      target_c2, hyst_db, p->d.min_hold_frames, p->d.xfade_frames, 1, p->mh_tf,
                      p->mh_cnt, p->mh_off, p->mh_sym, p->mh_soff, t_out, states, rows, alpha_out,
-                     spec ? p->mh_bs : nullptr);
+                     spec ? p->mh_bs : nullptr, p->mh_gtf, p->mh_gcnt, p->mh_goff);
   return launch_check();
 }
 
