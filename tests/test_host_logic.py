@@ -197,3 +197,15 @@ def test_level_nonmonotone_steps_are_isolated():
             bad.extend((b[np.nonzero(lv[1:] < lv[:-1])[0]]).tolist())
     assert 0 < len(bad) < 64
     assert np.min(np.diff(np.asarray(bad, np.int64))) > 4 * 8192
+
+
+def test_analysis_n_fft_bounds_host_side():
+    """analysis._check_n_fft (tm_analysis.hip's limits): powers of two in
+    [16, 16384], other lengths in [16, 8192] (Bluestein over >= 2n - 1 points
+    in LDS); refused before any device call."""
+    from tomatis_audio_processor_amd import analysis
+    for ok in (16, 17, 100, 1000, 3000, 4096, 8191, 8192, 16384):
+        analysis._check_n_fft(ok)
+    for bad in (1, 8, 15, 8193, 9000, 12000, 16383, 32768):
+        with pytest.raises(ValueError, match="n_fft"):
+            analysis._check_n_fft(bad)
