@@ -2074,6 +2074,7 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
       // workgroups per probe: a few segments each (one pass of the block's
       // threads over their (segment, start) pairs), at most 8
       p->mh_parts = std::max(1, std::min(8, (max_nseg * nsm + 767) / 768));
+      if (const int e = tshared::env_int("TOMATIS_MH_PARTS", 0)) p->mh_parts = std::max(1, std::min(32, e));
       if ((rc = dalloc_copy(&p->mh_goff, goff))) return rc;
       if (goff[ns] > 0) {
         if (hipMalloc(reinterpret_cast<void**>(&p->mh_gtf), goff[ns] * sizeof(uint16_t))) return TOMATIS_E_NOMEM;
