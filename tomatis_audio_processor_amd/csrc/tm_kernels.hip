@@ -1112,7 +1112,8 @@ __global__ __launch_bounds__(1024) void k_mh_probe(const double* __restrict__ le
     if (last && threadIdx.x == 0) arrive[(int64_t)s * kMhSlots + j] = 0;
     return;  // the final tables are read by k_minhold (next launch)
   }
-  __threadfence();
+  // the other workgroups' tables: agent-scope loads (no cache-wide acquire,
+  // which would invalidate this XCD's L2 under the concurrent probes)
   for (int e = threadIdx.x; e < nseg * ns; e += blockDim.x) {
     tf_l[e] = __hip_atomic_load(tf + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     cnt_l[e] = __hip_atomic_load(cn + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
