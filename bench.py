@@ -226,6 +226,9 @@ def main():
                          "PMC traffic runs)")
     ap.add_argument("--cpu-pool-s", type=int, default=300,
                     help="seconds of audio per worker for the all-cores CPU baseline")
+    ap.add_argument("--dev", action="append", default=[], metavar="NAME=VALUE",
+                    help="development override (TOMATIS_DEV_<NAME>, A/B experiments); "
+                         "recorded in the JSON line's config")
     a = ap.parse_args()
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
         raise SystemExit(relaunch(a.gpus))
@@ -237,6 +240,10 @@ def main():
     import torch.distributed as dist
     rank, ws, local = dist_init()
     from tomatis_audio_processor_amd import engine
+    from tomatis_audio_processor_amd._lib import set_dev_option
+    for kv in a.dev:
+        k, v = kv.split("=", 1)
+        set_dev_option(k.upper(), int(v))
 
     nstr, secs, sr, ch, mode, n_fft, hop, desc = WORKLOADS[a.workload]
     n = secs * sr
@@ -338,7 +345,8 @@ def main():
                        "channels": ch, "sr": sr, "mode": mode, "n_fft": n_fft, "hop": hop,
                        "parallelism": (f"time-sharded x{ws} (RCCL gate all_gather + peak "
                                        f"all_reduce)" if strong else
-                                       f"file-parallel x{ws} (RCCL manifest all_gather)")},
+                                       f"file-parallel x{ws} (RCCL manifest all_gather)"),
+                       **({"dev_overrides": a.dev} if a.dev else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,

@@ -272,11 +272,41 @@ int tomatis_plan_error_bits(tomatis_plan_t plan, uint32_t* bits, int32_t reset,
  *       the 7 midpoints of their tree, 7 workgroups per stream over the chip,
  *       when every stream's tables fit the LDS (else serial); 1: the 30 steps
  *       in one workgroup per stream -- the small footprint to prefer when the
- *       call overlaps another stream group's transform. */
+ *       call overlaps another stream group's transform.
+ *   TOMATIS_OPT_LIMITER_ROUNDS (0 auto / 1 / 2): the fused limiter of
+ *       standard-mode n_fft 2048 plans in two rounds (auto: on): round 1 leaves
+ *       its output unscaled, round 2 scales it block by block inside its own
+ *       frame loop, so only round 2's rescale is a tail.  Same results as 1. */
 #define TOMATIS_OPT_FUSE_LIMITER 1
 #define TOMATIS_OPT_LIMITER_SPIN 2
 #define TOMATIS_OPT_MINHOLD_SERIAL 3
+#define TOMATIS_OPT_LIMITER_ROUNDS 4
 int tomatis_plan_set_option(tomatis_plan_t plan, int32_t option, int64_t value);
+/* 2 when the plan's fused limiter runs in two rounds (TOMATIS_OPT_LIMITER_ROUNDS
+ * auto/2 and an eligible plan), else 1; -1 for a null plan. */
+int32_t tomatis_plan_limiter_rounds(tomatis_plan_t plan);
+
+/* Development overrides (tests and A/B experiments only).  Process-wide,
+ * explicit: the library reads no environment variable.  value < 0 restores the
+ * default.  Read at plan creation: FORCE_LDS, P64 (n_fft 2048 as one wave per
+ * frame), FAST_LOOP (interior loop), RUN_FRAMES (frames per run, 0 auto),
+ * RUN_ROUNDS, LEVELS_LEGACY, GATE_TF (transfer-function gate scan), MH_PARTS;
+ * at launch: GATE_TF, ALPHA_SEQ (sequential xfade alpha), GAIN_LDS,
+ * FUSE_LIMITER, WG (transform workgroup size).  Results are bit-identical
+ * under every value (the decomposition tests vary them). */
+#define TOMATIS_DEV_FAST_LOOP 1
+#define TOMATIS_DEV_RUN_ROUNDS 2
+#define TOMATIS_DEV_RUN_FRAMES 3
+#define TOMATIS_DEV_LEVELS_LEGACY 4
+#define TOMATIS_DEV_GATE_TF 5
+#define TOMATIS_DEV_MH_PARTS 6
+#define TOMATIS_DEV_FORCE_LDS 7
+#define TOMATIS_DEV_P64 8
+#define TOMATIS_DEV_ALPHA_SEQ 9
+#define TOMATIS_DEV_GAIN_LDS 10
+#define TOMATIS_DEV_FUSE_LIMITER 11
+#define TOMATIS_DEV_WG 12
+int tomatis_set_dev_option(int32_t key, int32_t value);
 
 /* max |x| over n floats as float bits (out zeroed by caller). */
 int tomatis_absmax(const float* x, int64_t n, uint32_t* out_bits, void* hip_stream);

@@ -36,6 +36,8 @@ def _run(mode, x, sr, **p):
 @pytest.mark.parametrize("n_fft,hop,secs", [
     (12000, 3000, 3.0),    # Bluestein, M = 32768: HBM buffers
     (32768, 8192, 4.0),    # power of two above the LDS: HBM buffers
+    (40000, 10000, 4.0),   # Bluestein, M = 131072: the largest HBM buffers
+    (65536, 16384, 4.0),   # kMaxNfft, power of two
     (100, 25, 0.5),        # Bluestein in LDS, M = 256
     (16, 4, 0.1),
     (3, 1, 0.02),

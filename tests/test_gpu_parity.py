@@ -220,19 +220,17 @@ def test_gate_paths_multistream(gate_path, up_delay_ms, monkeypatch):
     different lengths whose level toggles around the thresholds every few frames."""
     torch, E = _engine()
     from oracle import tomatis_oracle as orc
-    if gate_path == "tf":
-        monkeypatch.setenv("TOMATIS_GATE_TF", "1")
-    else:
-        monkeypatch.delenv("TOMATIS_GATE_TF", raising=False)
+    from tomatis_audio_processor_amd._lib import dev_options
     sr, rng = 44100, np.random.default_rng(int(up_delay_ms) + 7)
     xs = []
     for n in (sr * 20 + 77, sr * 9, sr * 31 + 1000):
         steps = np.repeat(10 ** (rng.uniform(-75, -5, n // 700 + 1) / 20), 700)[:n]
         xs.append((rng.standard_normal((n, 2)) * steps[:, None]).astype(np.float32))
     ss = E.StreamSet.from_arrays(xs, sr)
-    pipe = E.GatePipeline(ss, gate_ui=50, n_fft=2048, hop=512, up_delay_ms=up_delay_ms)
-    res = pipe.run()
-    torch.cuda.synchronize()
+    with dev_options(GATE_TF=1 if gate_path == "tf" else -1):
+        pipe = E.GatePipeline(ss, gate_ui=50, n_fft=2048, hop=512, up_delay_ms=up_delay_ms)
+        res = pipe.run()
+        torch.cuda.synchronize()
     for i in range(3):
         r = res.stream_r(i)
         starts = res.first_start[i] + 512 * np.arange(len(r), dtype=np.int64)
@@ -253,11 +251,12 @@ def test_fused_limiter_matches_two_pass(monkeypatch):
     xs = [(rng.standard_normal((n, 2)) * 0.3).astype(np.float32)
           for n in (sr * 40 + 5, sr * 13, sr * 27 + 999, sr * 6)]
     outs = []
-    for fuse in ("0", "1"):
-        monkeypatch.setenv("TOMATIS_FUSE_LIMITER", fuse)
-        ss = E.StreamSet.from_arrays(xs, sr)
-        pipe = E.GatePipeline(ss, gate_ui=50, n_fft=2048, hop=512)
-        res = pipe.run()
+    from tomatis_audio_processor_amd._lib import dev_options
+    for fuse in (0, 1):
+        with dev_options(FUSE_LIMITER=fuse):
+            ss = E.StreamSet.from_arrays(xs, sr)
+            pipe = E.GatePipeline(ss, gate_ui=50, n_fft=2048, hop=512)
+            res = pipe.run()
         torch.cuda.synchronize()
         pipe.plan.check_device()
         outs.append((res.y.cpu().numpy().copy(), res.chunk_peaks.cpu().numpy().copy()))

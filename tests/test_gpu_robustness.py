@@ -186,3 +186,57 @@ def test_c4_batch_per_gpu():
             rs = ref["scales"][c] or 1.0
             assert abs(gs / rs - 1) <= 5e-5, (i, c)
             assert np.abs(y[a:b][m[a:b]] - ref["y"][a:b][m[a:b]]).max() <= TOL, (i, c)
+
+
+def test_c5_batch_per_gpu():
+    """bench.py --workload c5 exactly as timed (one GPU's share of C5): 16 x
+    5 min stereo 96 kHz, xfade 500 ms (4096/1024) -> layer-2b residual EQ
+    (bench.ChainC5).  Stage 1: the per-chunk limiter property on all 16 streams;
+    4 streams vs orc.process_standard(xfade_ms=500) -- states and alpha bit-exact,
+    chunk scales within 5e-5, samples <= 1e-4 where sum w^2 >= 1e-3 (reference:
+    src/process_tomatis_xfade.py:206-219,251-312).  Stage 2 on the same 4:
+    orc.apply_residual_eq on the GPU's own stage-1 floats, samples <= 1e-4
+    (src/layer2b_apply_residual_eq.py:120-160)."""
+    torch, E = _engine()
+    import bench
+    S, secs, sr, ch, _, n_fft, hop, _ = bench.WORKLOADS["c5"]
+    n = secs * sr
+    ss = E.StreamSet.synthetic(S, n, ch, sr, seed0=1000)
+    chain = bench.ChainC5(E, ss, sr, n_fft, hop)
+    res2 = chain.run()
+    torch.cuda.synchronize()
+    res1 = chain.s1.result()
+    y_all = res1.y[:S * n * ch].view(S, n, ch)
+    ranges = res1.chunk_ranges(0)
+    assert all(res1.chunk_ranges(i) == ranges for i in range(S))
+    cmax = torch.stack([y_all[:, a:b].abs().amax(dim=(1, 2)) for a, b in ranges], 1).cpu().numpy()
+    for i in range(S):
+        peaks = res1.stream_peaks(i)
+        for c in range(len(ranges)):
+            assert cmax[i, c] <= LIM * (1 + 2e-7), (i, c, cmax[i, c])
+            if peaks[c] > LIM:
+                assert cmax[i, c] >= LIM * (1 - 1e-6), (i, c)
+    rf = np.geomspace(20.0, sr / 2, 400)
+    rd = 4.0 * np.sin(np.log2(rf / 20.0) * 1.7) * np.exp(-rf / 12000.0)
+    for i in (0, 5, 10, 15):
+        x = synth_stream(1000 + i, n, ch, sr)
+        ref = orc.process_standard(x, sr, gate_ui=50, gate_offset=-90, n_fft=n_fft, hop=hop,
+                                   xfade_ms=500.0)
+        np.testing.assert_array_equal(res1.stream_states(i), ref["states"])
+        np.testing.assert_array_equal(res1.stream_alpha(i), ref["alpha"])
+        y1 = res1.output(i)
+        m = ref["wsum"][ref["pad"]:ref["pad"] + n] >= TAU
+        flags = res1.scale_flags(i)
+        peaks = res1.stream_peaks(i)
+        for c, (a, b) in enumerate(ranges):
+            if flags[c]:
+                continue
+            gs = float(np.float32(LIM) / np.float32(peaks[c])) if peaks[c] > LIM else 1.0
+            rs = ref["scales"][c] or 1.0
+            assert abs(gs / rs - 1) <= 5e-5, (i, c)
+            assert np.abs(y1[a:b][m[a:b]] - ref["y"][a:b][m[a:b]]).max() <= TOL, (i, c)
+        y2 = res2.output(i)
+        r2 = orc.apply_residual_eq(y1, sr, rf, rd, n_fft=n_fft, hop=hop)
+        assert y2.shape == r2["y"].shape
+        m2 = r2["wsum"] >= TAU
+        assert np.abs(y2[m2] - r2["y"][m2]).max() <= TOL, i

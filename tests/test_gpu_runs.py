@@ -5,13 +5,11 @@ The host cuts every stream into interior runs (fast loop) and edge runs
 (tm_kernels.hip plan_build); the limiter is fused in-kernel or run as a second
 launch.  Every output hop block is the same frame-ordered float32 sum whatever
 the cut, so outputs, chunk peaks and states must be bitwise identical across:
-run lengths (TOMATIS_RUN_FRAMES), the interior loop on/off (TOMATIS_FAST_LOOP),
-and the fused/unfused limiter (TOMATIS_FUSE_LIMITER).  One small case is also
+run lengths (TOMATIS_DEV_RUN_FRAMES), the interior loop on/off
+(TOMATIS_DEV_FAST_LOOP), and the fused/unfused limiter (TOMATIS_DEV_FUSE_LIMITER).  One small case is also
 checked against the oracle.  Streams of unequal, odd lengths make frame_base
 odd for some streams (the gain-row ids are read as aligned 32-bit words).
 """
-import os
-
 import numpy as np
 import pytest
 
@@ -29,10 +27,13 @@ def _engine():
     return torch, engine
 
 
+def _dev(env):
+    from tomatis_audio_processor_amd._lib import dev_options
+    return dev_options(**{k.replace("TOMATIS_", ""): int(v) for k, v in env.items()})
+
+
 def _run(E, torch, xs, sr, env, **params):
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update({k: str(v) for k, v in env.items()})
-    try:
+    with _dev(env):
         ss = E.StreamSet.from_arrays(xs, sr)
         pipe = E.GatePipeline(ss, **params)
         res = pipe.run()
@@ -42,12 +43,6 @@ def _run(E, torch, xs, sr, env, **params):
         sts = [res.stream_states(i) for i in range(len(xs))]
         pks = [res.stream_peaks(i) for i in range(len(xs))]
         return outs, sts, pks
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
 
 
 @pytest.mark.parametrize("n_fft,hop,sr", [(2048, 512, 44100), (4096, 1024, 96000),
@@ -93,9 +88,7 @@ def test_xfade_alpha_parallel_matches_sequential(n_fft, hop, sr, xfade_ms):
     xs = [synth_stream(900 + i, n, 2, sr) for i, n in enumerate(lens)]
 
     def run(env):
-        old = {k: os.environ.get(k) for k in env}
-        os.environ.update({k: str(v) for k, v in env.items()})
-        try:
+        with _dev(env):
             ss = E.StreamSet.from_arrays(xs, sr)
             pipe = E.GatePipeline(ss, gate_ui=50, gate_offset=-90, n_fft=n_fft, hop=hop,
                                   xfade_ms=xfade_ms)
@@ -104,12 +97,6 @@ def test_xfade_alpha_parallel_matches_sequential(n_fft, hop, sr, xfade_ms):
             return ([res.stream_alpha(i) for i in range(len(xs))],
                     [res.output(i) for i in range(len(xs))],
                     pipe.rows[:pipe.plan.total_frames].cpu().numpy())
-        finally:
-            for k, v in old.items():
-                if v is None:
-                    os.environ.pop(k, None)
-                else:
-                    os.environ[k] = v
 
     a_seq, y_seq, r_seq = run({"TOMATIS_ALPHA_SEQ": 1})
     a_par, y_par, r_par = run({})

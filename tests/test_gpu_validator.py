@@ -1,0 +1,119 @@
+"""GPU: the reference validator's pass criteria on full-size (60 min) outputs
+of this build (the validator STFTs as on-box checks).
+
+``validate_layer1.py`` judges a processed file with two criteria:
+
+* gate (``:110-193,504``): an independent re-simulation of the gate from the
+  input -- levels of frames on an n_fft/2-padded grid, the hysteresis + up-delay
+  automaton on the frames that start inside the input -- against the state CSV
+  (states and levels); PASS when the mismatch rate is < 1 % and the largest
+  level difference < 0.1 dB.  The re-simulation here is the oracle's numpy
+  restatement (host, independent of the device); the "CSV" is this build's
+  device states and levels (r -> dBFS as the CLI writes them).  Checked on the
+  bench's own C2 input (BASELINE configs[1]).
+* spectrum (``:392-394,567-590``): per class (stable C1 / C2 frames with level
+  >= -60 dBFS) the median over frames of |Y| / |X|, in dB, against
+  ``build_tilt_gain_db``; PASS when the RMSE in 100-800, 800-1200 and
+  2000-8000 Hz is < 1.5 dB for both classes.  The criterion measures the
+  filter, so it needs an input the per-chunk limiter leaves alone (a limited
+  chunk shifts its whole curve by 20 log10(scale), for the reference as for
+  this build): the same 60-min synthetic noise re-enveloped to -30 / -50 dBFS
+  (loud / quiet halves), which keeps both classes above the -60 dBFS level
+  gate; the test asserts that no chunk was limited.
+"""
+import numpy as np
+import pytest
+
+from oracle import tomatis_oracle as orc
+
+pytestmark = pytest.mark.gpu
+SR, SECS, NFFT, HOP = 44100, 3600, 2048, 512
+
+
+def _engine():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from tomatis_audio_processor_amd import analysis, dsp, engine
+    return torch, engine, analysis, dsp
+
+
+def _csv_rows(n, first_start, n_frames):
+    """Frames whose start lies in [0, n): the rows the CLI writes to the CSV
+    (process_tomatis.py:408-409)."""
+    k = np.arange(n_frames)
+    s = first_start + k * HOP
+    return k[(s >= 0) & (s < n)]
+
+
+def test_validator_gate_criterion_c2_fullsize():
+    torch, E, _, _ = _engine()
+    n = SR * SECS
+    ss = E.StreamSet.synthetic(1, n, 2, SR, seed0=1000)  # bench.py's C2 input
+    pipe = E.GatePipeline(ss, gate_ui=50, n_fft=NFFT, hop=HOP)
+    res = pipe.run()
+    torch.cuda.synchronize()
+    st = pipe.streams[0]
+    rows = _csv_rows(n, st.first_start, st.n_frames)
+    csv_states = res.stream_states(0)[rows]
+    csv_levels = orc.r_to_level(res.stream_r(0)[rows])
+    # validate_layer1.simulate_gate: pad n_fft/2 both sides, frames at k*hop
+    # while k*hop + n_fft <= len(x_pad), the automaton only on frames whose
+    # original start is inside x (starting from C1, no pending)
+    x = ss.x[:n * 2].cpu().numpy().reshape(n, 2)
+    pad = NFFT // 2
+    xp = np.zeros((n + 2 * pad, 2), np.float32)
+    xp[pad:pad + n] = x
+    del x
+    Fv = (len(xp) - NFFT) // HOP + 1
+    kv = np.arange(Fv)
+    inside = (kv * HOP - pad >= 0) & (kv * HOP - pad < n)
+    lv = orc.r_to_level(orc.frame_r(orc.frame_view(xp, NFFT, HOP, Fv)))[inside]
+    del xp
+    ud = int(250.0 * SR / 1000)
+    sim = orc.gate_standard(lv, kv[inside] * HOP, pipe.Ton, pipe.Toff, ud)
+    m = min(len(sim), len(csv_states))
+    assert m > 0.99 * len(csv_states)
+    mismatch = float(np.mean(sim[:m] != csv_states[:m]))
+    level_diff = float(np.max(np.abs(lv[:m] - csv_levels[:m])))
+    assert mismatch < 0.01, mismatch        # validate_layer1.py:504
+    assert level_diff < 0.1, level_diff
+    # both classes occur (the criterion is not vacuous)
+    assert 0.05 < float(np.mean(csv_states == 2)) < 0.95
+
+
+def test_validator_spectrum_criterion_fullsize():
+    torch, E, A, dsp = _engine()
+    n = SR * SECS
+    ss = E.StreamSet.synthetic(1, n, 2, SR, seed0=1000)
+    # re-envelope the synthetic noise: loud half (-20 dBFS) -> -30, quiet half
+    # (-60 dBFS) -> -50 (phase of synth.envelope: quiet first, 1.5 s each)
+    idx = torch.arange(n, device=ss.x.device)
+    half = (3 * SR) // 2
+    g = torch.where(torch.remainder(idx, 3 * SR) < half,
+                    torch.tensor(10.0 ** (10 / 20), device=ss.x.device),
+                    torch.tensor(10.0 ** (-10 / 20), device=ss.x.device)).to(torch.float32)
+    x2 = ss.x[:n * 2].view(n, 2) * g[:, None]
+    del idx, g
+    ss2 = E.StreamSet(x=x2.reshape(-1).contiguous(), offs=[0], lens=[n], ch=2, sr=SR)
+    pipe = E.GatePipeline(ss2, gate_ui=50, n_fft=NFFT, hop=HOP)
+    res = pipe.run()
+    torch.cuda.synchronize()
+    assert float(res.stream_peaks(0).max()) <= 0.999, "a limited chunk would bias the curves"
+    st = pipe.streams[0]
+    rows = _csv_rows(n, st.first_start, st.n_frames)
+    states = ["C1" if s == 1 else "C2" for s in res.stream_states(0)[rows].tolist()]
+    y = res.y[:n * 2].view(n, 2)
+    freqs, c1_db, c2_db, n1, n2 = A.compute_conditional_spectrum(
+        ss2.x.view(n, 2), y, SR, states, NFFT, HOP, level_threshold=-60)
+    assert n1 > 1000 and n2 > 1000, (n1, n2)
+    th1 = dsp.build_tilt_gain_db(freqs, 1000.0, 12.0, 15.0, -15.0)
+    th2 = dsp.build_tilt_gain_db(freqs, 1000.0, 12.0, -15.0, 15.0)
+
+    def rmse(meas, th, lo, hi):  # validate_layer1.compute_spectrum_rmse
+        m = (freqs >= lo) & (freqs <= hi)
+        return float(np.sqrt(np.mean((meas[m] - th[m]) ** 2)))
+
+    bands = [(100, 800), (800, 1200), (2000, 8000)]
+    worst = max(rmse(c, t, lo, hi) for c, t in ((c1_db, th1), (c2_db, th2)) for lo, hi in bands)
+    assert worst < 1.5, worst                # validate_layer1.py:588-589

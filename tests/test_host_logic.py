@@ -209,3 +209,18 @@ def test_analysis_n_fft_bounds_host_side():
     for bad in (1, 8, 15, 8193, 9000, 12000, 16383, 32768):
         with pytest.raises(ValueError, match="n_fft"):
             analysis._check_n_fft(bad)
+
+
+def test_levels_threaded_inside_host_pool_no_deadlock(monkeypatch):
+    """host_levels runs on _host_pool(); its float64 branch splits the
+    log10 chain into slices.  With one pool worker the slices must not queue
+    behind their own caller (they run on a separate executor)."""
+    import concurrent.futures as cf
+    from tomatis_audio_processor_amd import dsp, engine
+    monkeypatch.setenv("TOMATIS_LOG10_THREADS", "4")
+    monkeypatch.setattr(engine, "_POOL", cf.ThreadPoolExecutor(max_workers=1))
+    r = np.random.default_rng(3).random(1 << 17) * 0.5
+    out = np.empty(len(r), np.float64)
+    fut = engine._host_pool().submit(engine._levels_threaded, r, out)
+    fut.result(timeout=60)
+    assert np.array_equal(out, dsp.r_to_level(r))

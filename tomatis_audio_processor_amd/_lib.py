@@ -22,6 +22,10 @@ ERR_PAIR_BARRIER = 2     # TOMATIS_ERR_PAIR_BARRIER
 OPT_FUSE_LIMITER = 1     # TOMATIS_OPT_FUSE_LIMITER
 OPT_LIMITER_SPIN = 2     # TOMATIS_OPT_LIMITER_SPIN
 OPT_MINHOLD_SERIAL = 3   # TOMATIS_OPT_MINHOLD_SERIAL
+OPT_LIMITER_ROUNDS = 4   # TOMATIS_OPT_LIMITER_ROUNDS
+# development overrides (TOMATIS_DEV_*: tests and A/B experiments only)
+DEV_KEYS = dict(FAST_LOOP=1, RUN_ROUNDS=2, RUN_FRAMES=3, LEVELS_LEGACY=4, GATE_TF=5, MH_PARTS=6,
+                FORCE_LDS=7, P64=8, ALPHA_SEQ=9, GAIN_LDS=10, FUSE_LIMITER=11, WG=12)
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 F32, F64 = 0, 1
@@ -97,6 +101,8 @@ _SIGS = {
     "tomatis_plan_error": (C.c_int, [_P, _P]),
     "tomatis_plan_error_bits": (C.c_int, [_P, C.POINTER(C.c_uint32), C.c_int32, _P]),
     "tomatis_plan_set_option": (C.c_int, [_P, C.c_int32, C.c_int64]),
+    "tomatis_plan_limiter_rounds": (C.c_int32, [_P]),
+    "tomatis_set_dev_option": (C.c_int, [C.c_int32, C.c_int32]),
     "tomatis_absmax": (C.c_int, [_P, C.c_int64, _P, _P]),
     "tomatis_absmax_streams": (C.c_int, [_P, _P, _P, _P]),
     "tomatis_scale_copy": (C.c_int, [_P, _P, C.c_int64, C.c_float, _P]),
@@ -172,3 +178,27 @@ def ptr(t) -> C.c_void_p:
 def stream_handle(device=None) -> C.c_void_p:
     import torch
     return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def set_dev_option(name: str, value: int):
+    """tomatis_set_dev_option(TOMATIS_DEV_<name>, value); value < 0 restores
+    the default.  Process-wide; the library reads no environment variable."""
+    check(lib().tomatis_set_dev_option(DEV_KEYS[name], int(value)), "set_dev_option")
+
+
+class dev_options:
+    """Context manager: ``with dev_options(RUN_FRAMES=48, FAST_LOOP=0): ...``
+    sets development overrides and restores the defaults on exit."""
+
+    def __init__(self, **kw):
+        self.kw = kw
+
+    def __enter__(self):
+        for k, v in self.kw.items():
+            set_dev_option(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k in self.kw:
+            set_dev_option(k, -1)
+        return False

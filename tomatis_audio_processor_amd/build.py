@@ -39,21 +39,36 @@ FLAGS = [ARCH, "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "
          "-I" + os.path.join(ROOT, "include")]
 
 
-def needs_build() -> bool:
-    if not os.path.exists(OUT):
-        return True
-    t = os.path.getmtime(OUT)
-    return any(os.path.getmtime(d) > t for d in DEPS)
+def _unit_cmd(src: str, fl, extra, obj: str):
+    return [HIPCC, *FLAGS, *fl, *extra, "-c", "-o", obj + ".tmp", os.path.join(CSRC, src)]
 
 
-def _stale(obj: str, src: str) -> bool:
-    """A unit recompiles when its object is missing or older than its source,
-    a shared header or this script (objects are kept next to the library)."""
-    if not os.path.exists(obj):
+def _unit_hash(src: str, cmd) -> str:
+    """Content hash of a unit: its full command line (minus the output path),
+    its source and every shared header -- an object whose recorded hash
+    differs is rebuilt (flags changed, or an edit landed during a build)."""
+    import hashlib
+    h = hashlib.sha256(" ".join(cmd[:-3] + cmd[-1:]).encode())
+    for d in [os.path.join(CSRC, src)] + [d for d in DEPS if not d.endswith(".hip")]:
+        with open(d, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def _stale(obj: str, src: str, cmd) -> bool:
+    """A unit recompiles when its object is missing or its recorded hash
+    (objects and hashes are kept next to the library) differs."""
+    if not os.path.exists(obj) or not os.path.exists(obj + ".hash"):
         return True
-    t = os.path.getmtime(obj)
-    deps = [os.path.join(CSRC, src)] + [d for d in DEPS if not d.endswith(".hip")]
-    return any(os.path.getmtime(d) > t for d in deps)
+    with open(obj + ".hash") as f:
+        return f.read().strip() != _unit_hash(src, cmd)
+
+
+def needs_build(out: str = OUT) -> bool:
+    if not os.path.exists(out):
+        return True
+    return any(_stale(f"{out}.{src}.o", src, _unit_cmd(src, fl, (), f"{out}.{src}.o"))
+               for src, fl in UNITS.items())
 
 
 def build(force: bool = False, verbose: bool = True, out: str = OUT, extra=()) -> str:
@@ -64,17 +79,20 @@ def build(force: bool = False, verbose: bool = True, out: str = OUT, extra=()) -
     for src, fl in UNITS.items():
         obj = f"{out}.{src}.o"
         objs.append(obj)
-        if not force and not extra and not _stale(obj, src):
+        cmd = _unit_cmd(src, fl, extra, obj)
+        if not force and not extra and not _stale(obj, src, cmd):
             continue
-        cmd = [HIPCC, *FLAGS, *fl, *extra, "-c", "-o", obj + ".tmp", os.path.join(CSRC, src)]
+        digest = _unit_hash(src, cmd)  # of the inputs as compiled (before the compile)
         if verbose:
             print(" ".join(cmd), flush=True)
-        procs.append((subprocess.Popen(cmd), obj))
-    rcs = [p.wait() for p, _ in procs]
+        procs.append((subprocess.Popen(cmd), obj, digest))
+    rcs = [p.wait() for p, _, _ in procs]
     if any(rcs):
         raise subprocess.CalledProcessError(max(rcs), "hipcc")
-    for _, obj in procs:
+    for _, obj, digest in procs:
         os.replace(obj + ".tmp", obj)
+        with open(obj + ".hash", "w") as f:
+            f.write(digest + "\n")
     link = [HIPCC, ARCH, "-shared", "-fPIC", "-o", out + ".tmp", *objs]
     if verbose:
         print(" ".join(link), flush=True)
@@ -83,6 +101,8 @@ def build(force: bool = False, verbose: bool = True, out: str = OUT, extra=()) -
     if extra or out != OUT:
         for o in objs:
             os.remove(o)
+            if os.path.exists(o + ".hash"):
+                os.remove(o + ".hash")
     return out
 
 

@@ -149,7 +149,9 @@ struct BitReader {
 constexpr int kBlock = 4096;
 constexpr int kMaxPart = 8;
 
-inline uint64_t zz(int64_t r) { return (uint64_t)((r << 1) ^ (r >> 63)); }
+// zigzag (the shift in unsigned arithmetic: left-shifting a negative value is
+// undefined before C++20; found by the UBSan sweep, tools/flac_sanitize.cpp)
+inline uint64_t zz(int64_t r) { return ((uint64_t)r << 1) ^ (uint64_t)(r >> 63); }
 
 void fixed_residual(const int64_t* s, int n, int order, int64_t* r) {
   for (int i = order; i < n; ++i) {
@@ -547,24 +549,30 @@ int decode_frame(const uint8_t* d, size_t len, size_t p, int ch0, int bps0, int6
           }
           if (r.bad) return TOMATIS_FLAC_E_FORMAT;
         }
-        // prediction
+        // prediction, in wrapping unsigned arithmetic: a valid stream never
+        // overflows (same results), a corrupt one (rejected by the CRC-16 below)
+        // must not reach signed-overflow UB first (UBSan sweep,
+        // tools/flac_sanitize.cpp)
         if (lpc) {
           for (int t = order; t < n; ++t) {
-            int64_t acc = 0;
-            for (int j = 0; j < order; ++j) acc += coef[j] * s[t - 1 - j];
-            s[t] += acc >> shift;
+            uint64_t acc = 0;
+            for (int j = 0; j < order; ++j) acc += (uint64_t)coef[j] * (uint64_t)s[t - 1 - j];
+            s[t] = (int64_t)((uint64_t)s[t] + (uint64_t)((int64_t)acc >> shift));
           }
         } else {
           for (int t = order; t < n; ++t) {
-            int64_t pr;
+            uint64_t pr;
+            const uint64_t a1 = (uint64_t)s[t - (order > 0 ? 1 : 0)];
             switch (order) {
               case 0: pr = 0; break;
-              case 1: pr = s[t - 1]; break;
-              case 2: pr = 2 * s[t - 1] - s[t - 2]; break;
-              case 3: pr = 3 * s[t - 1] - 3 * s[t - 2] + s[t - 3]; break;
-              default: pr = 4 * s[t - 1] - 6 * s[t - 2] + 4 * s[t - 3] - s[t - 4]; break;
+              case 1: pr = a1; break;
+              case 2: pr = 2 * a1 - (uint64_t)s[t - 2]; break;
+              case 3: pr = 3 * a1 - 3 * (uint64_t)s[t - 2] + (uint64_t)s[t - 3]; break;
+              default:
+                pr = 4 * a1 - 6 * (uint64_t)s[t - 2] + 4 * (uint64_t)s[t - 3] - (uint64_t)s[t - 4];
+                break;
             }
-            s[t] += pr;
+            s[t] = (int64_t)((uint64_t)s[t] + pr);
           }
         }
       } else {
@@ -586,7 +594,7 @@ int decode_frame(const uint8_t* d, size_t len, size_t p, int ch0, int bps0, int6
     if (asg == 8) b = a - b;                 // left, side -> right
     else if (asg == 9) a = a + b;            // side, right -> left
     else if (asg == 10) {                    // mid, side
-      const int64_t m = (a << 1) | (b & 1);
+      const int64_t m = (int64_t)(((uint64_t)a << 1) | (uint64_t)(b & 1));
       a = (m + b) >> 1;
       b = (m - b) >> 1;
     }

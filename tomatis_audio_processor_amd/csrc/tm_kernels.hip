@@ -1112,8 +1112,15 @@ __global__ __launch_bounds__(1024) void k_mh_probe(const double* __restrict__ le
     if (last && threadIdx.x == 0) arrive[(int64_t)s * kMhSlots + j] = 0;
     return;  // the final tables are read by k_minhold (next launch)
   }
-  // the other workgroups' tables: agent-scope loads (no cache-wide acquire,
-  // which would invalidate this XCD's L2 under the concurrent probes)
+  // the other workgroups' tables.  Ordering: every producer's tables are
+  // released by its __threadfence() before its arrival; the acquire side is
+  // thread 0's agent-scope ACQ_REL fetch_add above (it MUST stay acq_rel: a
+  // relaxed arrival would let these loads see stale tables, and the
+  // speculative and serial bisections would then differ only intermittently),
+  // extended to the other threads by the __syncthreads() after it; the loads
+  // are agent scope (served by L2, never a stale L1 line).  No extra
+  // cache-wide acquire fence: it would invalidate this CU's L1 under the
+  // concurrent probes for nothing.
   for (int e = threadIdx.x; e < nseg * ns; e += blockDim.x) {
     tf_l[e] = __hip_atomic_load(tf + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     cnt_l[e] = __hip_atomic_load(cn + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1531,6 +1538,7 @@ struct tomatis_plan_s {
   TomatisStream* st = nullptr;
   Run* runs = nullptr;
   int n_runs = 0;
+  std::vector<Run> hruns;  // host copy of the runs
   LvlBlock* lblocks = nullptr;
   int n_lblocks = 0;
   GateSeg* segs = nullptr;
@@ -1576,6 +1584,15 @@ struct tomatis_plan_s {
   int edge_mask = 0;      // set for one tomatis_stft_ola_limited_edges call
   int fuse_enabled = 1;   // TOMATIS_OPT_FUSE_LIMITER
   int lim_spin = 1 << 18; // TOMATIS_OPT_LIMITER_SPIN: fused-limiter wait bound (polls)
+  // two-round fused limiter (TOMATIS_OPT_LIMITER_ROUNDS): runs
+  // [0, n1) are round 1, [n1, n_runs) round 2; partner[r] = the round-1 run whose
+  // output round-2 run r scales; chunk_final[g] = no round-2 contributions
+  int lim_rounds = 0;     // option: 0 auto, 1 off, 2 on
+  int n1 = 0;             // > 0: the plan's runs are laid out for two rounds
+  int32_t* partner = nullptr;
+  uint32_t* chunk_final = nullptr;
+  uint32_t* pieces = nullptr;
+  int max_pieces = 0;
   // run-scan gate (exclusive on/off predicates)
   bool gate_excl = false;
   void* gsum = nullptr;
@@ -1630,9 +1647,12 @@ int launch_check() { return hipfail(hipGetLastError()); }
 }  // namespace
 
 namespace tshared {
-int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : dflt;
+// development overrides (tomatis_set_dev_option); -1 = the default
+constexpr int kDevKeys = 13;
+static int g_dev[kDevKeys] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+int dev_opt(int key, int dflt) {
+  const int v = (key > 0 && key < kDevKeys) ? g_dev[key] : -1;
+  return v < 0 ? dflt : v;
 }
 }  // namespace tshared
 
@@ -1659,6 +1679,7 @@ int tomatis_plan_destroy(tomatis_plan_t p) {
                   p->grp_base, p->leaf_base, p->leaves, p->gsum, p->gcarry, p->gcarry_in,
                   p->aq, p->afin, p->acin,
                   p->chunk_need, p->chunk_done, p->chunk_rng, p->err, p->twL,
+                  p->partner, p->chunk_final, p->pieces,
                   p->pw_leaf, p->pw_prog, p->blue_b, p->blue_h, p->glb_work};
   for (void* q : ptrs) dfree(q);
   delete p;
@@ -1686,15 +1707,18 @@ static bool gate_exclusive(const TomatisStream& S) {
   return true;
 }
 
-// in-place iterative radix-2 FFT in double (plan set-up: Bluestein filter)
-static int plan_build(tomatis_plan_s* p, const float* window) {
+// Runs of the fused kernel (plan creation, and again when
+// TOMATIS_OPT_LIMITER_ROUNDS changes the layout), then the fused-limiter
+// accounting that depends on them.
+static int build_runs(tomatis_plan_s* p) {
   const TomatisPlanDesc& d = p->d;
   const int N = d.n_fft, hop = d.hop, P = p->P;
-  int rc;
   const int ns = p->n_streams;
-  // --- stream table ---
-  if ((rc = dalloc_copy(&p->st, p->hs))) return rc;
-  // --- main-kernel runs ---
+  int rc;
+  // two-round fused limiter: standard-mode register plans (two gain rows, LDS),
+  // n_fft 2048 (the interior loop); TOMATIS_OPT_LIMITER_ROUNDS 1 turns it off
+  const bool two = !p->generic && P == 64 && d.alpha_mode == 0 && p->total_chunks > 0 &&
+                   p->lim_rounds != 1 && N <= 2048;
   const int64_t tf_total = std::max<int64_t>(1, p->total_frames);
   // Runs.  Per stream, the emitted frames [e_lo, e_hi) whose run can take the
   // fused kernel's interior loop (full frame loads back to the warm-up frames,
@@ -1704,7 +1728,7 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
   // blocks, every wave busy to the end), at least 48 frames per interior run
   // so the rmax-1 warm-up frames per run stay a few percent.
   const int rmax_ = (N + hop - 1) / hop;
-  const bool fast_ok = !p->generic && P == 64 && env_int("TOMATIS_FAST_LOOP", 1) != 0;
+  const bool fast_ok = !p->generic && P == 64 && dev_opt(TOMATIS_DEV_FAST_LOOP, 1) != 0;
   std::vector<int64_t> e_lo(ns, 0), e_hi(ns, 0);
   int64_t fast_total = 0, n_edge = 0;
   for (int s = 0; s < ns; ++s) {
@@ -1748,9 +1772,8 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
   // runs still compute, and their limiter rescale overlaps that compute
   // (adaptive: every stream is one limiter chunk, measured 1.4 ms faster on C3
   // with 2 rounds; standard 10 s chunks gain nothing and pay warm-up frames)
-  const int rounds =
-      std::max(1, env_int("TOMATIS_RUN_ROUNDS", (d.alpha_mode == 2 && ns > 1) ? 2 : 1));
-  int T = env_int("TOMATIS_RUN_FRAMES", 0);
+  const int rounds = std::max(1, dev_opt(TOMATIS_DEV_RUN_ROUNDS, (two || (d.alpha_mode == 2 && ns > 1)) ? 2 : 1));
+  int T = dev_opt(TOMATIS_DEV_RUN_FRAMES, 0);
   if (T <= 0) {
     // generic streams and the edge runs take slots first
     int64_t gen_frames = 0;
@@ -1796,7 +1819,99 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
     if (e_hi[s] < F) add_runs(s, e_hi[s], F, 0);
   }
   p->n_runs = (int)runs.size();
+  dfree(p->runs);
+  p->runs = nullptr;
   if ((rc = dalloc_copy(&p->runs, runs))) return rc;
+  p->hruns = runs;
+  p->n1 = 0;
+  if (two) {  // round 1 = the first half of the runs (stream / position order)
+    p->n1 = p->n_runs / 2;
+    if (p->n1 == 0) p->n1 = 0;
+  }
+  return TOMATIS_OK;
+}
+
+// Fused-limiter accounting over the plan's runs: flushes expected per chunk
+// (host mirror of the kernel's frame-indexed chunk walk), the largest run span
+// of a chunk, and for the two-round layout the partner of every round-2 run,
+// the chunks round 1 completes and the round-2 piece lists.
+static int limiter_accounting(tomatis_plan_s* p) {
+  if (p->generic || p->total_chunks <= 0) return TOMATIS_OK;
+  const int HOP = p->d.hop, wpr = p->P / 64;
+  const std::vector<Run>& runs = p->hruns;
+  int rc;
+  std::vector<uint32_t> need(p->total_chunks, 0);
+  std::vector<int32_t> first_run(p->total_chunks, -1), last_run(p->total_chunks, -1);
+  for (int ri = 0; ri < (int)runs.size(); ++ri) {
+    const Run& R = runs[ri];
+    const TomatisStream& S = p->hs[R.s];
+    const int64_t s_ka = S.first_start + R.ka * HOP;
+    int cid = 0;
+    if (S.n_chunks > 1 && s_ka >= S.chunk_first)
+      cid = (int)std::min<int64_t>(1 + (s_ka - S.chunk_first) / S.chunk_len, S.n_chunks - 1);
+    int64_t next_k = INT64_MAX;
+    if (S.n_chunks > 1 && cid < S.n_chunks - 1)
+      next_k = (S.chunk_first + (int64_t)cid * S.chunk_len - S.first_start) / HOP;
+    const int64_t step = S.n_chunks > 1 ? S.chunk_len / HOP : 0;
+    auto mark = [&](int c) {
+      const int g = S.chunk_base + c;
+      need[g] += wpr;
+      if (first_run[g] < 0) first_run[g] = ri;
+      last_run[g] = ri;
+    };
+    while (next_k < R.kb) {
+      if (next_k >= R.ka) {
+        mark(cid);
+        ++cid;
+        next_k = (cid < S.n_chunks - 1) ? next_k + step : INT64_MAX;
+      } else {
+        break;  // cannot happen: next chunk starts after the run's first frame
+      }
+    }
+    mark(cid);
+  }
+  int span = 0;
+  for (int g = 0; g < p->total_chunks; ++g)
+    if (first_run[g] >= 0) span = std::max(span, last_run[g] - first_run[g] + 1);
+  p->fuse_span = span;
+  dfree(p->chunk_need);
+  p->chunk_need = nullptr;
+  if ((rc = dalloc_copy(&p->chunk_need, need))) return rc;
+  dfree(p->partner);
+  dfree(p->chunk_final);
+  dfree(p->pieces);
+  p->partner = nullptr;
+  p->chunk_final = nullptr;
+  p->pieces = nullptr;
+  p->max_pieces = 0;
+  if (p->n1 > 0) {
+    const int nr = (int)runs.size(), n1 = p->n1, n2 = nr - n1;
+    std::vector<int32_t> partner(nr, -1);
+    for (int i = 0; i < n1 && i < n2; ++i) partner[n1 + i] = i;
+    std::vector<uint32_t> fin(p->total_chunks, 0);
+    for (int g = 0; g < p->total_chunks; ++g) fin[g] = (last_run[g] >= 0 && last_run[g] < n1) ? 1u : 0u;
+    int mp = 1;
+    for (int ri = n1; ri < nr; ++ri)
+      mp = std::max<int>(mp, (int)(runs[ri].kb - std::max<int64_t>(0, runs[ri].ka - (p->rmax - 1))));
+    p->max_pieces = mp;
+    if ((rc = dalloc_copy(&p->partner, partner))) return rc;
+    if ((rc = dalloc_copy(&p->chunk_final, fin))) return rc;
+    if (hipMalloc(reinterpret_cast<void**>(&p->pieces),
+                  (size_t)std::max(1, n2) * 2 * (mp + 1) * sizeof(uint32_t)))
+      return TOMATIS_E_NOMEM;
+  }
+  return TOMATIS_OK;
+}
+
+// in-place iterative radix-2 FFT in double (plan set-up: Bluestein filter)
+static int plan_build(tomatis_plan_s* p, const float* window) {
+  const TomatisPlanDesc& d = p->d;
+  const int N = d.n_fft, hop = d.hop, P = p->P;
+  int rc;
+  const int ns = p->n_streams;
+  // --- stream table ---
+  if ((rc = dalloc_copy(&p->st, p->hs))) return rc;
+  if ((rc = build_runs(p))) return rc;
   // --- levels: any n_fft (numpy pairwise program) ---
   // k_levels holds a block's span in LDS (f64: half as many samples); frames
   // that do not fit, and every n_fft that is not a power of two >= 256, take
@@ -1840,7 +1955,7 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
   }
   // --- streaming levels: leaves of 128 samples aligned to first_start ---
   p->leaf_path = (hop % 128 == 0) && N >= 256 && N <= 4096 && (N & (N - 1)) == 0 &&
-                 (d.ch == 1 || d.ch == 2) && env_int("TOMATIS_LEVELS_LEGACY", 0) == 0;
+                 (d.ch == 1 || d.ch == 2) && dev_opt(TOMATIS_DEV_LEVELS_LEGACY, 0) == 0;
   if (p->leaf_path) {
     std::vector<int64_t> gb(ns + 1, 0), lbase(ns + 1, 0);
     for (int s = 0; s < ns; ++s) {
@@ -1873,7 +1988,7 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
     }
     p->n_segs = (int)sg.size();
     if ((rc = dalloc_copy(&p->segs, sg))) return rc;
-    p->gate_excl = env_int("TOMATIS_GATE_TF", 0) == 0;
+    p->gate_excl = dev_opt(TOMATIS_DEV_GATE_TF, 0) == 0;
     for (int s = 0; s < ns; ++s) p->gate_excl = p->gate_excl && gate_exclusive(p->hs[s]);
     if (p->n_segs > 0) {
       if (hipMalloc(&p->gsum, (size_t)p->n_segs * 5 * sizeof(int))) return TOMATIS_E_NOMEM;
@@ -1946,7 +2061,12 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
       }
       if (M > kLdsMaxM && p->total_frames > 0) {
         const int64_t items = p->total_frames * ((d.ch + 1) / 2);
-        p->glb_blocks = (int)std::min<int64_t>(items, 512);
+        // one 1024-thread block per CU keeps the chip busy; each owns two
+        // M-element buffers (2 MiB at M = 131072)
+        int dev = 0, ncu = 256;
+        if (hipGetDevice(&dev) == hipSuccess)
+          (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        p->glb_blocks = (int)std::min<int64_t>(items, std::max(1, ncu));
         if (hipMalloc(reinterpret_cast<void**>(&p->glb_work),
                       (size_t)p->glb_blocks * 2 * M * sizeof(float2)))
           return TOMATIS_E_NOMEM;
@@ -1983,54 +2103,18 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
     p->total_out = tot;
     if ((rc = dalloc_copy(&p->chunks, cd))) return rc;
     if ((rc = dalloc_copy(&p->pos_base, pb))) return rc;
-    // fused limiter: flushes expected per chunk (host mirror of the kernel's
-    // frame-indexed chunk walk), chunk output ranges, eligibility
+    // fused limiter: chunk output ranges (the per-run accounting: build_runs)
     if (!p->generic && p->total_chunks > 0) {
-      const int HOP = hop, wpr = P / 64;
-      std::vector<uint32_t> need(p->total_chunks, 0);
       std::vector<int64_t> rng(2 * (size_t)p->total_chunks, 0);
       for (const ChunkDesc& C : cd) {
         rng[2 * (p->hs[C.s].chunk_base + C.c)] = C.p0;
         rng[2 * (p->hs[C.s].chunk_base + C.c) + 1] = C.p1;
       }
-      std::vector<int32_t> first_run(p->total_chunks, -1), last_run(p->total_chunks, -1);
-      for (int ri = 0; ri < (int)runs.size(); ++ri) {
-        const Run& R = runs[ri];
-        const TomatisStream& S = p->hs[R.s];
-        const int64_t s_ka = S.first_start + R.ka * HOP;
-        int cid = 0;
-        if (S.n_chunks > 1 && s_ka >= S.chunk_first)
-          cid = (int)std::min<int64_t>(1 + (s_ka - S.chunk_first) / S.chunk_len, S.n_chunks - 1);
-        int64_t next_k = INT64_MAX;
-        if (S.n_chunks > 1 && cid < S.n_chunks - 1)
-          next_k = (S.chunk_first + (int64_t)cid * S.chunk_len - S.first_start) / HOP;
-        const int64_t step = S.n_chunks > 1 ? S.chunk_len / HOP : 0;
-        auto mark = [&](int c) {
-          const int g = S.chunk_base + c;
-          need[g] += wpr;
-          if (first_run[g] < 0) first_run[g] = ri;
-          last_run[g] = ri;
-        };
-        while (next_k < R.kb) {
-          if (next_k >= R.ka) {
-            mark(cid);
-            ++cid;
-            next_k = (cid < S.n_chunks - 1) ? next_k + step : INT64_MAX;
-          } else {
-            break;  // cannot happen: next chunk starts after the run's first frame
-          }
-        }
-        mark(cid);
-      }
-      int span = 0;
-      for (int g = 0; g < p->total_chunks; ++g)
-        if (first_run[g] >= 0) span = std::max(span, last_run[g] - first_run[g] + 1);
-      p->fuse_span = span;
-      if ((rc = dalloc_copy(&p->chunk_need, need))) return rc;
       if ((rc = dalloc_copy(&p->chunk_rng, rng))) return rc;
       if (hipMalloc(reinterpret_cast<void**>(&p->chunk_done), (size_t)p->total_chunks * 4))
         return TOMATIS_E_NOMEM;
     }
+    if ((rc = limiter_accounting(p))) return rc;
     if (hipMalloc(reinterpret_cast<void**>(&p->err), 4)) return TOMATIS_E_NOMEM;
     if (hipMemset(p->err, 0, 4)) return TOMATIS_E_HIP;
   }
@@ -2075,7 +2159,7 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
       // workgroups per probe: a few segments each (one pass of the block's
       // threads over their (segment, start) pairs), at most 8
       p->mh_parts = std::max(1, std::min(8, (max_nseg * nsm + 767) / 768));
-      if (const int e = tshared::env_int("TOMATIS_MH_PARTS", 0)) p->mh_parts = std::max(1, std::min(32, e));
+      if (const int e = tshared::dev_opt(TOMATIS_DEV_MH_PARTS, 0)) p->mh_parts = std::max(1, std::min(32, e));
       if ((rc = dalloc_copy(&p->mh_goff, goff))) return rc;
       if (goff[ns] > 0) {
         if (hipMalloc(reinterpret_cast<void**>(&p->mh_gtf), goff[ns] * sizeof(uint16_t))) return TOMATIS_E_NOMEM;
@@ -2110,14 +2194,14 @@ int tomatis_plan_create(tomatis_plan_t* out, const TomatisPlanDesc* desc, const 
   // register kernels: n_fft 2048 / 4096 with <= 2 channels (L + iR); every
   // other n_fft or more channels: the any-size path (Stockham FFT of length M,
   // Bluestein when n_fft is not a power of two)
-  p->lds = !(N == 2048 || N == 4096) || d.ch > 2 || env_int("TOMATIS_FORCE_LDS", 0) != 0;
+  p->lds = !(N == 2048 || N == 4096) || d.ch > 2 || dev_opt(TOMATIS_DEV_FORCE_LDS, 0) != 0;
   if (p->lds) {
     p->blue = (N & (N - 1)) != 0;
     int M = 1;
     while (M < (p->blue ? 2 * N - 1 : N)) M <<= 1;
     p->lds_M = M;
   }
-  p->P = p->lds ? 64 : ((N == 2048 && env_int("TOMATIS_P64", 1)) ? 64 : 128);
+  p->P = p->lds ? 64 : ((N == 2048 && dev_opt(TOMATIS_DEV_P64, 1)) ? 64 : 128);
   p->NR = N / p->P;
   p->SH = (!p->lds && hop % p->P == 0) ? hop / p->P : 0;
   p->generic = p->lds || (p->NR == 16 ? !(p->SH == 2 || p->SH == 4 || p->SH == 8)
@@ -2167,7 +2251,7 @@ int tomatis_plan_update_streams(tomatis_plan_t p, const TomatisStream* streams, 
         a.chunk_len != b.chunk_len || a.n_chunks != b.n_chunks)
       return TOMATIS_E_ARG;
   }
-  bool excl = env_int("TOMATIS_GATE_TF", 0) == 0;
+  bool excl = dev_opt(TOMATIS_DEV_GATE_TF, 0) == 0;
   for (int i = 0; i < p->n_streams; ++i) {
     TomatisStream s = streams[i];
     s.frame_base = p->hs[i].frame_base;
@@ -2290,7 +2374,7 @@ int tomatis_gate_std(tomatis_plan_t p, const float* r, uint8_t* states, uint16_t
   }
   if (xf) {
     const int nxf = p->d.xfade_frames;
-    if (env_int("TOMATIS_ALPHA_SEQ", 0) != 0) {
+    if (dev_opt(TOMATIS_DEV_ALPHA_SEQ, 0) != 0) {
       hipLaunchKernelGGL(k_alpha_xfade, dim3((p->n_streams + 63) / 64), dim3(64), 0, s, p->st,
                          p->n_streams, states, nxf, rows, alpha_out);
       return launch_check();
@@ -2503,7 +2587,7 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
   A.edge_mask = p->edge_mask;
   A.lds_row[0] = 0;
   A.lds_row[1] = 1;
-  if (n_rows > 2 && N <= 2048 && p->d.alpha_mode != 0 && env_int("TOMATIS_GAIN_LDS", 1) != 0) {
+  if (n_rows > 2 && N <= 2048 && p->d.alpha_mode != 0 && dev_opt(TOMATIS_DEV_GAIN_LDS, 1) != 0) {
     // cross-fade tables: the pure rows (alpha 0 and 1) carry most frames
     // (xfade: rows 0/1; adaptive: rows 2 and 2 + xfade_frames = n_rows - 1)
     A.n_rows_lds = 2;
@@ -2520,6 +2604,11 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
   A.err = p->err;
   A.lim_spin = p->lim_spin;
   A.prof = nullptr;
+  A.run_base = 0;
+  A.defer_self = 0;
+  A.partner = nullptr;
+  A.pieces = nullptr;
+  A.max_pieces = 0;
   if (limit > 0.f) {
     if (!p->chunk_done) return TOMATIS_E_UNSUPPORTED;
     if (hipMemsetAsync(p->chunk_done, 0, (size_t)p->total_chunks * 4, s)) return TOMATIS_E_HIP;
@@ -2554,6 +2643,28 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
   }
   return launch_check();
 #endif
+  // two-round fused limiter: round 1 leaves its output unscaled; k_r2_plan lists
+  // the round-1 blocks each round-2 run scales inside its frame loop (chunks
+  // complete after round 1); round 2 then runs with its partners (two-row LDS
+  // gain tables only, the kernel's GM 1 instantiation)
+  if (limit > 0.f && p->n1 > 0 && p->partner && A.n_rows_lds > 0 && !A.lds_mixed) {
+    MainArgs A1 = A;
+    A1.n_runs = p->n1;
+    A1.defer_self = 1;
+    launch_transform(A1, p->P, p->NR, p->SH, ch, transform_wg(p->P, p->NR), s);
+    int rc = launch_check();
+    if (rc) return rc;
+    MainArgs A2 = A;
+    A2.run_base = p->n1;
+    A2.n_runs = p->n_runs - p->n1;
+    A2.partner = p->partner;
+    A2.pieces = p->pieces;
+    A2.max_pieces = p->max_pieces;
+    launch_r2_plan(A2, p->chunk_final, p->pieces, s);
+    if ((rc = launch_check())) return rc;
+    launch_transform(A2, p->P, p->NR, p->SH, ch, transform_wg(p->P, p->NR), s);
+    return launch_check();
+  }
   launch_transform(A, p->P, p->NR, p->SH, ch, transform_wg(p->P, p->NR), s);
   return launch_check();
 }
@@ -2589,7 +2700,7 @@ int tomatis_stft_ola_limited_edges(tomatis_plan_t p, const float* x, const float
                                    uint32_t* peaks, float limit, int32_t edge_mask, void* hs) {
   if (!p || !(limit > 0.f) || edge_mask < 0 || edge_mask > 3) return TOMATIS_E_ARG;
   const bool fuse = !p->generic && p->chunk_done && p->fuse_span > 0 && p->fuse_enabled &&
-                    p->fuse_span <= fuse_max_span(p) && env_int("TOMATIS_FUSE_LIMITER", 1) != 0;
+                    p->fuse_span <= fuse_max_span(p) && dev_opt(TOMATIS_DEV_FUSE_LIMITER, 1) != 0;
   p->edge_mask = edge_mask;
   int rc;
   if (fuse) {
@@ -2637,8 +2748,28 @@ int tomatis_plan_set_option(tomatis_plan_t p, int32_t option, int64_t value) {
       p->lim_spin = (int)value;
       return TOMATIS_OK;
     case TOMATIS_OPT_MINHOLD_SERIAL: p->mh_serial = value != 0; return TOMATIS_OK;
+    case TOMATIS_OPT_LIMITER_ROUNDS: {
+      if (value < 0 || value > 2) return TOMATIS_E_ARG;
+      if (p->lim_rounds == (int)value) return TOMATIS_OK;
+      p->lim_rounds = (int)value;
+      if (p->n_streams == 0 || p->lds) return TOMATIS_OK;
+      int rc = build_runs(p);
+      if (!rc) rc = limiter_accounting(p);
+      return rc;
+    }
     default: return TOMATIS_E_ARG;
   }
+}
+
+int tomatis_set_dev_option(int32_t key, int32_t value) {
+  if (key <= 0 || key >= tshared::kDevKeys) return TOMATIS_E_ARG;
+  tshared::g_dev[key] = value < 0 ? -1 : value;
+  return TOMATIS_OK;
+}
+
+int32_t tomatis_plan_limiter_rounds(tomatis_plan_t p) {
+  if (!p) return -1;
+  return (p->n1 > 0 && p->partner) ? 2 : 1;
 }
 
 int tomatis_apply_limiter(tomatis_plan_t p, float* y, const uint32_t* peaks, float limit, void* hs) {

@@ -57,7 +57,21 @@ struct MainArgs {
   uint32_t* err;        // TOMATIS_ERR_* bits
   int lim_spin;         // fused-limiter wait bound (polls of the chunk counter)
   unsigned long long* prof;  // TM_PROFILE builds only: per-phase wave cycles
+  // Two-round fused limiter (DESIGN.md §6 "Limiter rounds"): round 1 writes its
+  // output unscaled (defer_self: no rescale tail); in round 2 every run also
+  // scales the output of partner[run] (a round-1 run, -1: none): the hop blocks
+  // k_r2_plan listed (chunks complete after round 1 whose peak exceeds the
+  // limit) inside its frame loop, the rest in its tail.
+  int run_base;         // this launch runs [run_base, run_base + n_runs)
+  int defer_self;
+  const int32_t* partner;   // round 2 only, indexed by run
+  // round 2: per launched run 2 * (max_pieces + 1) words: {count, first block
+  // left to the tail}, then count x {partner block, scale bits}
+  const uint32_t* pieces;
+  int max_pieces;
 };
+void launch_r2_plan(const MainArgs& A, const uint32_t* chunk_final, uint32_t* pieces,
+                    hipStream_t s);
 
 // Any-size path (any n_fft in [2, kMaxNfft], any hop, 1..kMaxCh channels): per
 // (frame, channel pair) a Stockham FFT of length M (n_fft when it is a power
@@ -99,6 +113,6 @@ void launch_gain_perm(int P, int NR, const float* gains, int n_rows, int n_bins,
                       hipStream_t s);
 void launch_ola_gather(const MainArgs& A, int n_streams, const int64_t* pos_base, int64_t total,
                        int N, hipStream_t s);
-int env_int(const char* name, int dflt);
+int dev_opt(int key, int dflt);  // tomatis_set_dev_option (default when unset)
 
 }  // namespace tshared

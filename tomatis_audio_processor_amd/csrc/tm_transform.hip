@@ -190,7 +190,9 @@ typedef __attribute__((address_space(4))) const uint32_t cu32;
 // GM: where the gain rows live (per-lane layout).  0: global (L2) only;
 // 1: all (<= 2) rows in LDS; 2: the two pure rows A.lds_row[0..1] in LDS, the
 // cross-fade lattice rows from global (row is wave-uniform, so is the branch).
-template <int P, int NR, int SH, int CH, int GM, bool PF, bool NT, int WG>
+// PR: round 2 of the two-round fused limiter (MainArgs::partner): each interior
+// run also rescales its round-1 partner's output inside its frame loop.
+template <int P, int NR, int SH, int CH, int GM, bool PF, bool NT, int WG, bool PR = false>
 __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(MainArgs A) {
 #ifdef TM_PROFILE
   const unsigned long long t_k0 = __builtin_amdgcn_s_memtime();
@@ -210,6 +212,8 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   __shared__ __attribute__((aligned(16))) float s_winv[SHQ * P];  // lane-quad layout
   __shared__ cf s_buf[NSEQ][G::SEQ_LDS];
   __shared__ __attribute__((aligned(16))) float s_gain[GM ? 2 * N : 4];
+  // PR: one hop block per sequence for the partner rescale (LDS-DMA target)
+  __shared__ __attribute__((aligned(16))) char s_pbuf[PR ? NSEQ * SH * P * CH * 4 : 16];
   for (int i = threadIdx.x; i < NR * P; i += WG) s_twN[i] = A.twN[i];
   if constexpr (LT) {  // [m/2][l][m&1] = W_P^{(l%8)*m}
     for (int i = threadIdx.x; i < 8 * P; i += WG) {
@@ -247,9 +251,10 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
 
   const int seq = threadIdx.x / P, L = threadIdx.x % P;
   // wave-uniform run id (readfirstlane: run and stream descriptors load as scalars)
-  const int run_id = __builtin_amdgcn_readfirstlane(blockIdx.x * NSEQ + seq);
+  const int run_loc = __builtin_amdgcn_readfirstlane(blockIdx.x * NSEQ + seq);
+  const int run_id = A.run_base + run_loc;
   Run R{0, 0, 0, 0};
-  const bool valid = run_id < A.n_runs;
+  const bool valid = run_loc < A.n_runs;
   if (valid) R = A.runs[run_id];
   if constexpr (P <= 64) {
     if (!valid) return;
@@ -372,6 +377,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
 
   bool fast_run = false;
   if constexpr (P == 64) fast_run = valid && (R.last & kRunInterior);
+  int p_done = 0;  // PR: partner blocks [0, p_done) handled in the frame loop
   if (fast_run) {
     // Interior run (host-marked): every frame of [kfirst, kb) reads a full frame
     // and every emitted hop block is a full interior block (no stream edges, no
@@ -424,6 +430,35 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       }
     };
     cf v[NR], nh[SH], o[SH];
+    // ---- round 2: rescale the partner's (round-1 run) blocks in this loop ----
+    // k_r2_plan listed, for this run, the partner's hop blocks to scale (chunks
+    // round 1 completed whose peak exceeds the limit) with their scale, at most
+    // one per frame: frame it loads piece it into this sequence's LDS slot by
+    // LDS-DMA at its top and scales and stores it at its end (no VGPRs in
+    // flight across the transform, which is at its register limit).
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    constexpr int HOPB = HOP * CH * 4;
+    constexpr int BQ = PR ? HOPB / 1024 : 1;  // b128 per lane per block
+    static_assert(!PR || HOPB % 1024 == 0, "a hop block is whole b128 per lane");
+    // (wave-uniform values made explicit: a VGPR resource or LDS address here
+    // becomes a waterfall loop)
+    char* const pslot = s_pbuf + (PR ? __builtin_amdgcn_readfirstlane(seq * HOPB) : 0);
+    cu32* plist = nullptr;
+    int np = 0;
+    float* yP = ys;
+    if constexpr (PR) {
+      const int pr = __builtin_amdgcn_readfirstlane(A.partner[run_id]);
+      plist = (cu32*)(A.pieces) + (int64_t)run_loc * 2 * (A.max_pieces + 1);
+      np = (int)plist[0];
+      if (np > 0) {
+        const Run RP = A.runs[pr];
+        const TomatisStream SP = A.st[RP.s];
+        const int64_t off = SP.out_off + CH * (SP.first_start + RP.ka * HOP - SP.out_begin);
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)off);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)off >> 32));
+        yP = A.y + (int64_t)(((uint64_t)hi << 32) | lo);
+      }
+    }
     uint32_t rw_nx = row_word(0);
     {  // frame 0, null stores (the loop's issue pattern), new hop of frame 1
       ld_old(0, v);
@@ -440,6 +475,18 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       const uint32_t row = row_of(rw_nx, it);
       rw_nx = row_word(min(it + 1, nit - 1));
       const bool emit = it >= nwarm;
+      if constexpr (PR) {
+        // piece it of the partner -> LDS slot (branch-free: past the list the
+        // resource is empty, the load returns zeros and the store drops)
+        const int blk = (int)plist[2 + 2 * min(it, np)];
+        const __amdgpu_buffer_rsrc_t rpl =
+            mk_rsrc(yP + (int64_t)blk * (HOP * CH), it < np ? (uint32_t)HOPB : 0u);
+#pragma unroll
+        for (int u = 0; u < BQ; ++u)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              rpl, (__attribute__((address_space(3))) void*)(pslot + u * 1024), 16, L * 16,
+              u * 1024, 0, 2);
+      }
       TPROF(0, v[0].x);
       transform(v, row);
       TPROF(5, v[NR - 1].x);
@@ -478,8 +525,29 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       for (int j = 0; j < SH; ++j) v[NO + j] = cf{opaque_f(nh[j].x), opaque_f(nh[j].y)};
       store_out(o, emit ? ry : rnull, emit ? (it - nwarm) * (HOP * CH * 4) : 0);
       ld_new(min(it + 2, nit - 1), nh);
+      if constexpr (PR) {
+        // piece it: scale, store (its LDS-DMA is counted by vmcnt only)
+        // behind this frame's critical loads: only ld_old / store_out / ld_new
+        // (NO + 2 SH instructions) were issued after the LDS-DMA, so this count
+        // waits for the DMA (counted by vmcnt only) and nothing issued later
+        constexpr int kAfter = NO + 2 * SH;
+        static_assert(kAfter < 63, "vmcnt range");
+        __asm__ volatile("s_waitcnt vmcnt(%0)" ::"n"(kAfter) : "memory");
+        const int blk = (int)plist[2 + 2 * min(it, np)];
+        const float sc = __uint_as_float(plist[3 + 2 * min(it, np)]);
+        const __amdgpu_buffer_rsrc_t rps =
+            mk_rsrc(yP + (int64_t)blk * (HOP * CH), it < np ? (uint32_t)HOPB : 0u);
+#pragma unroll
+        for (int u = 0; u < BQ; ++u) {
+          const f4v t = *reinterpret_cast<const f4v*>(pslot + u * 1024 + L * 16) * sc;
+          const f32x4 b = {__float_as_uint(t.x), __float_as_uint(t.y), __float_as_uint(t.z),
+                           __float_as_uint(t.w)};
+          __builtin_amdgcn_raw_buffer_store_b128(b, rps, L * 16, u * 1024, 2);
+        }
+      }
       TPROF(6, acc[0].x);
     }
+    if constexpr (PR) p_done = (int)plist[1];  // first block the frame loop left
 #ifdef TM_PROFILE
     if (L == 0) {
       for (int i = 0; i < 7; ++i) atomicAdd(A.prof + i, tacc[i]);
@@ -579,7 +647,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
     }
   }
   if (valid) flush_peak<P>(pk, cid, S, A.peaks, L, done);
-  if (valid && done) {
+  if (valid && done && !A.defer_self) {
     // this wave's own output range (stores of frames [ka, kb) and the stream tail)
     const int64_t s_last = S.first_start + (R.kb - 1) * HOP;
     const int64_t lo = max(s_ka, S.out_begin) - S.out_begin;
@@ -595,6 +663,28 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       limit_own<CH>(A, S, S.chunk_base + c, wlo, whi, L & 63);
     }
   }
+  if constexpr (PR) {  // the partner's output not scaled in the frame loop
+    const int pr = valid ? A.partner[run_id] : -1;
+    if (pr >= 0 && done) {
+      const Run RP = A.runs[pr];
+      const TomatisStream SP = A.st[RP.s];
+      const int64_t s_kaP = SP.first_start + RP.ka * HOP;
+      const int64_t s_lastP = SP.first_start + (RP.kb - 1) * HOP;
+      const int64_t endP = SP.out_begin + SP.out_len;
+      const int64_t lo = max(s_kaP + (int64_t)p_done * HOP, SP.out_begin) - SP.out_begin;
+      const int64_t hi = min(s_lastP + ((RP.last & 1) ? (int64_t)N : (int64_t)HOP), endP) - SP.out_begin;
+      if (lo < hi) {
+        const int nw = P / 64, w = L >> 6;
+        const int64_t span = hi - lo, per = (span + nw - 1) / nw;
+        const int64_t wlo = lo + per * w, whi = min(hi, wlo + per);
+        const int c0 = chunk_of(lo + SP.out_begin, SP), c1 = chunk_of(hi - 1 + SP.out_begin, SP);
+        for (int c = c0; c <= c1; ++c) {
+          if (((A.edge_mask & 1) && c == 0) || ((A.edge_mask & 2) && c == SP.n_chunks - 1)) continue;
+          limit_own<CH>(A, SP, SP.chunk_base + c, wlo, whi, L & 63);
+        }
+      }
+    }
+  }
 #ifdef TM_PROFILE
   if (valid && (R.last & kRunInterior) && L == 0) {
     const unsigned long long t_k2 = __builtin_amdgcn_s_memtime();
@@ -605,6 +695,79 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
     atomicAdd(A.prof + 10, 1ull);          // waves
   }
 #endif
+}
+
+// Round 2 of the two-round fused limiter: for each run of the launch, the hop
+// blocks of its round-1 partner that its frame loop scales (one per frame):
+// blocks of chunks with no round-2 contributions (chunk_final) whose peak
+// exceeds the limit, in order, up to the first chunk that round 2 still
+// completes or the run's frame count.  Scale = limit / peak in float32, as the
+// limiter (src/process_tomatis.py:351-355).
+__global__ __launch_bounds__(64) void k_r2_plan(MainArgs A, const uint32_t* __restrict__ chunk_final,
+                                                uint32_t* __restrict__ out) {
+  // one wave per run; lanes take the partner's blocks 64 at a time
+  const int t = blockIdx.x, lane = threadIdx.x;
+  if (t >= A.n_runs) return;
+  uint32_t* o = out + (int64_t)t * 2 * (A.max_pieces + 1);
+  const int run = A.run_base + t;
+  const int pr = A.partner[run];
+  int n = 0, stop = 0;
+  if (pr >= 0 && (A.runs[pr].last & kRunInterior) && (A.runs[run].last & kRunInterior)) {
+    const Run R = A.runs[run], RP = A.runs[pr];
+    const TomatisStream SP = A.st[RP.s];
+    const int hop = A.hop;
+    const int nit = (int)(R.kb - max<int64_t>(0, R.ka - (A.rmax - 1)));
+#ifdef TM_DEV_R2_TAIL_ONLY  // experiment: every partner block left to the tail
+    const int cap = 0;
+#else
+    const int cap = min(nit, A.max_pieces);
+#endif
+    const int nb = (int)(RP.kb - RP.ka);
+    const int64_t s0 = SP.first_start + RP.ka * hop;
+    stop = nb;
+    for (int j0 = 0; j0 < nb && j0 < stop; j0 += 64) {
+      const int j = j0 + lane;
+      bool want = false, halt = false;
+      float sc = 1.f;
+      if (j < nb) {
+        const int c = chunk_of(s0 + (int64_t)j * hop, SP);
+        const int g = SP.chunk_base + c;
+        halt = !chunk_final[g] ||
+               ((A.edge_mask & 1) && c == 0) || ((A.edge_mask & 2) && c == SP.n_chunks - 1);
+        if (!halt) {
+          const float peak = __uint_as_float(A.peaks[g]);
+          want = peak > A.limit;
+          sc = A.limit / peak;
+        }
+      }
+      // the walk ends at the first block of a chunk round 2 completes (or an edge chunk)
+      const uint64_t hb = __ballot(halt);
+      const int first_halt = hb ? j0 + __builtin_ctzll(hb) : INT_MAX;
+      want = want && j < first_halt;
+      const uint64_t wb = __ballot(want);
+      const int before = __builtin_popcountll(wb & ((1ull << lane) - 1ull));
+      if (want && n + before < cap) {
+        o[2 + 2 * (n + before)] = (uint32_t)j;
+        o[3 + 2 * (n + before)] = __float_as_uint(sc);
+      }
+      const int cnt = __builtin_popcountll(wb);
+      if (n + cnt > cap) {
+        // the frame loop is full: the tail takes the rest from the first block left
+        const int k = cap - n;  // wanted blocks of this batch that fit
+        uint64_t m = wb;
+        for (int i = 0; i < k; ++i) m &= m - 1;
+        stop = min(stop, j0 + __builtin_ctzll(m));
+        n = cap;
+        break;
+      }
+      n += cnt;
+      if (first_halt != INT_MAX) stop = min(stop, first_halt);
+    }
+  }
+  if (lane == 0) {
+    o[0] = (uint32_t)n;
+    o[1] = (uint32_t)stop;
+  }
 }
 
 // Generic hop: same transform, windowed frame outputs to scratch, then a gather.
@@ -942,6 +1105,13 @@ void launch_main_pf(const MainArgs& A, int ch, hipStream_t s) {
   constexpr bool kNoLdsGains = P == 128 && NR == 32;
   const int gm = kNoLdsGains ? 0 : (A.n_rows_lds > 0 ? (A.lds_mixed ? 2 : 1) : 0);
   const dim3 g((A.n_runs + WG / P - 1) / (WG / P)), b(WG);
+  if constexpr (P == 64 && WG == 512) {
+    if (A.partner) {  // round 2 of the two-round limiter (two-row tables: gm == 1)
+      if (ch == 2) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 1, PF, NT, WG, true>), g, b, 0, s, A);
+      else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, 1, PF, NT, WG, true>), g, b, 0, s, A);
+      return;
+    }
+  }
 #ifdef TM_DEV_ONE_KERNEL  // dev/asm studies: one instantiation (stereo, LDS gains)
   (void)gm;
   (void)ch;
@@ -977,7 +1147,9 @@ void launch_main(const MainArgs& A, int ch, int wg, hipStream_t s) {
   return launch_main_pf<P, NR, SH, false, true, TM_DEV_WG>(A, ch, s);
 #endif
   if constexpr (P == 64) {
-    if (wg == 512) return launch_main_pf<P, NR, SH, false, true, 512>(A, ch, s);
+    // round 2 of the two-round limiter: 512-thread blocks (the per-sequence LDS
+    // slots of the partner rescale fit once per CU)
+    if (wg == 512 || A.partner) return launch_main_pf<P, NR, SH, false, true, 512>(A, ch, s);
     return launch_main_pf<P, NR, SH, false, true, 256>(A, ch, s);
   }
   if constexpr (P == 128 && NR == 32) {
@@ -1004,7 +1176,7 @@ int transform_wg(int P, int NR) {
   // same occupancy with one copy of the tables; measured equal).
   // P = 128, NR = 32 (n_fft 4096): 4 two-wave sequences (~120 KB, 2 waves/SIMD).
   const int dflt = P == 64 ? 256 : (NR == 32 ? 512 : 256);
-  const int w = env_int("TOMATIS_WG", dflt);
+  const int w = dev_opt(TOMATIS_DEV_WG, dflt);
   if (P == 64 && (w == 256 || w == 512)) return w;
   if (P == 128 && NR == 32 && (w == 256 || w == 512)) return w;
   if (P == 128 && NR == 16 && (w == 256 || w == 512 || w == 768)) return w;
@@ -1075,6 +1247,12 @@ void launch_lds_frames(const LdsArgs& A, hipStream_t s) {
   LDS_M(1024) LDS_M(2048) LDS_M(4096) LDS_M(8192) LDS_M(16384)
 #endif
 #undef LDS_M
+}
+
+void launch_r2_plan(const MainArgs& A, const uint32_t* chunk_final, uint32_t* pieces,
+                    hipStream_t s) {
+  if (A.n_runs <= 0) return;
+  hipLaunchKernelGGL(k_r2_plan, dim3(A.n_runs), dim3(64), 0, s, A, chunk_final, pieces);
 }
 
 void launch_lds_gather(const LdsArgs& A, hipStream_t s) {

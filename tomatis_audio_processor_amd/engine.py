@@ -27,7 +27,7 @@ import numpy as np
 
 from . import dsp
 from ._lib import (ERR_LIMITER_WAIT, ERR_PAIR_BARRIER, F32, F64, NORM_EPS, NORM_MAX,
-                   OPT_FUSE_LIMITER, OPT_LIMITER_SPIN, OPT_MINHOLD_SERIAL, TomatisPlanDesc, TomatisStream, check, lib,
+                   OPT_FUSE_LIMITER, OPT_LIMITER_ROUNDS, OPT_LIMITER_SPIN, OPT_MINHOLD_SERIAL, TomatisPlanDesc, TomatisStream, check, lib,
                    ptr, stream_handle)
 
 PEAK_LIMIT = 0.999
@@ -111,6 +111,7 @@ class Plan:
                                     win.ctypes.data_as(C.POINTER(C.c_float)),
                                     self.streams, self.n), "plan_create")
         self.h = h
+        self._opts = {}
         self.total_frames = int(L.tomatis_plan_total_frames(h))
         self.total_chunks = int(L.tomatis_plan_total_chunks(h))
 
@@ -132,6 +133,21 @@ class Plan:
 
     def set_option(self, option: int, value: int):
         check(self.L.tomatis_plan_set_option(self.h, option, int(value)), "plan_set_option")
+        self._opts[option] = int(value)
+
+    def option(self, option: int, default: int) -> int:
+        """The value this wrapper last set for ``option`` (else ``default``)."""
+        return self._opts.get(option, default)
+
+    def set_limiter_rounds(self, rounds: int):
+        """TOMATIS_OPT_LIMITER_ROUNDS: 0 auto, 1 one round, 2 two rounds (the
+        round-1 output is scaled inside round 2's frame loop)."""
+        self.set_option(OPT_LIMITER_ROUNDS, rounds)
+
+    @property
+    def limiter_rounds(self) -> int:
+        """2 when this plan's fused limiter runs in two rounds, else 1."""
+        return int(self.L.tomatis_plan_limiter_rounds(self.h))
 
     def set_limiter_spin(self, polls: int):
         """Fused-limiter wait bound (fault injection: 0 forces the recovery path)."""
@@ -174,11 +190,12 @@ def finish_plan(plan: Plan, redo, what: str) -> int:
         warnings.warn(f"{what}: fused limiter wait timed out on the device; "
                       "re-running the transform with the separate limiter launch",
                       RuntimeWarning, stacklevel=3)
+        prev = plan.option(OPT_FUSE_LIMITER, 1)  # the caller's setting is restored
         plan.set_option(OPT_FUSE_LIMITER, 0)
         try:
             redo()
         finally:
-            plan.set_option(OPT_FUSE_LIMITER, 1)
+            plan.set_option(OPT_FUSE_LIMITER, prev)
         again = plan.error_bits(reset=True)
         if again:
             raise DeviceCheckError(f"{what}: device error bits {again:#x} after the unfused re-run")
@@ -224,7 +241,23 @@ def _levels_threaded(r: np.ndarray, out: np.ndarray, tmp: np.ndarray = None):
         part(0, n)
         return
     edges = np.linspace(0, n, k + 1).astype(np.int64)
-    list(_host_pool().map(lambda i: part(edges[i], edges[i + 1]), range(k)))
+    # the slices go to their own executor: callers run on _host_pool() (a stream
+    # group's host_levels task), and slices queued behind their own caller on
+    # that pool would never start once every worker waits
+    list(_slice_pool(k).map(lambda i: part(edges[i], edges[i + 1]), range(k)))
+
+
+_SLICE_POOL = None
+
+
+def _slice_pool(k: int):
+    """Workers for the log10 slices of _levels_threaded only (never the pool
+    its callers run on)."""
+    global _SLICE_POOL
+    if _SLICE_POOL is None or _SLICE_POOL._max_workers < k:
+        import concurrent.futures as cf
+        _SLICE_POOL = cf.ThreadPoolExecutor(max_workers=max(1, min(16, k)))
+    return _SLICE_POOL
 
 
 def _set_gate(st: TomatisStream, Ton: float, Toff: float):
