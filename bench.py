@@ -4,9 +4,11 @@
 Default workload (BASELINE.json configs[1], "C2"): one 60-min stereo 44.1 kHz
 stream per GPU, standard mode (process_tomatis), n_fft=2048, hop=512, Hann,
 gate_ui=50 (log_percent, -40 dBFS), +-15 dB tilt.  A step = one pass of the
-whole device chain over the resident input: levels -> gate scan (3 kernels) ->
-fused STFT-gain-ISTFT-OLA-normalise -> limiter fix-up.  Input is seeded
-synthetic PCM generated on the device before timing.
+whole device chain over the resident input: the gate look-back pre-kernel, then
+the fused levels -> gate -> STFT-gain-ISTFT-OLA-normalise -> per-chunk limiter
+kernel (tomatis_stft_ola_gated; shapes it declines run levels -> gate scan ->
+fused transform + limiter).  Input is seeded synthetic PCM generated on the
+device before timing.
 
 Contract: `python bench.py --gpus N --steps K --warmup W`; for N > 1 launched
 by torch.distributed.run (one rank per GPU, RCCL).  Multi-GPU = weak scaling:
@@ -346,6 +348,7 @@ def main():
                        "parallelism": (f"time-sharded x{ws} (RCCL gate all_gather + peak "
                                        f"all_reduce)" if strong else
                                        f"file-parallel x{ws} (RCCL manifest all_gather)"),
+                       "fused_levels": bool(getattr(pipe, "gated_used", False)),
                        **({"dev_overrides": a.dev} if a.dev else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",

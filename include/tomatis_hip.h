@@ -239,6 +239,24 @@ int tomatis_stft_ola_limited_edges(tomatis_plan_t plan, const float* x, const fl
                                    int32_t n_rows, const uint16_t* rows, float* y,
                                    uint32_t* chunk_peak_bits, float limit, int32_t edge_mask,
                                    void* hip_stream);
+/* tomatis_levels(F32) + tomatis_gate_std + tomatis_stft_ola_limited in one
+ * pass over the input (standard mode): a small pre-kernel finds every run's
+ * gate state before its first frame (a look-back to the nearest frame that
+ * fixes the automaton's state: one not "on" and "off", or up_delay_frames + 1
+ * consecutive "on" and not "off"), then the transform kernel computes each
+ * frame's r (numpy's pairwise order, bit-identical to tomatis_levels) and
+ * state from the samples it loads for the FFT and picks the gain row from it.
+ * r_out (f32) and states_out (1 = C1, 2 = C2) per frame as tomatis_levels /
+ * tomatis_gate_std write them; n_rows must be 2 (rows C1, C2); limit 0 = no
+ * limiter.  TOMATIS_E_UNSUPPORTED unless n_fft 2048, hop 256 or 512, <= 2
+ * channels, alpha_mode 0, in_scale 1 and every stream below 2^31 bytes (the
+ * caller runs the two-pass chain).  When a run's look-back does not resolve
+ * within 512 frames the launch sets TOMATIS_ERR_GATE_CARRY and its outputs are
+ * invalid: the caller re-runs the two-pass chain.  Replaces
+ * src/process_tomatis.py:373-385 (levels + gate loop) feeding :391-400. */
+int tomatis_stft_ola_gated(tomatis_plan_t plan, const float* x, const float* gain_rows,
+                           int32_t n_rows, float* y, uint32_t* chunk_peak_bits, float limit,
+                           float* r_out, uint8_t* states_out, void* hip_stream);
 /* The limiter on the edge chunks of edge_mask only. */
 int tomatis_apply_limiter_edges(tomatis_plan_t plan, float* y, const uint32_t* chunk_peak_bits,
                                 float limit, int32_t edge_mask, void* hip_stream);
@@ -251,12 +269,18 @@ int tomatis_apply_limiter_edges(tomatis_plan_t plan, float* y, const uint32_t* c
  *       TOMATIS_OPT_FUSE_LIMITER = 0 (transform, then tomatis_apply_limiter).
  *   TOMATIS_ERR_PAIR_BARRIER  a two-wave (n_fft 4096) exchange barrier timed
  *       out: that launch's FFTs are wrong; no retry makes it safe.
+ *   TOMATIS_ERR_GATE_CARRY  tomatis_stft_ola_gated could not resolve a run's
+ *       gate carry-in within its look-back (the level stayed between the two
+ *       thresholds, never D + 1 frames above): that launch's states and output
+ *       are invalid; re-run the two-pass path (tomatis_levels, tomatis_gate_std,
+ *       tomatis_stft_ola_limited), which has no look-back limit.
  * Synchronous: tomatis_plan_error returns TOMATIS_E_HIP if any bit is set
  * since creation (or the last reset), else OK; tomatis_plan_error_bits returns
  * the bits and clears them when reset != 0.  Replaces nothing in the
  * reference (its loop has no asynchronous device work to check). */
 #define TOMATIS_ERR_LIMITER_WAIT 1u
 #define TOMATIS_ERR_PAIR_BARRIER 2u
+#define TOMATIS_ERR_GATE_CARRY 4u
 int tomatis_plan_error(tomatis_plan_t plan, void* hip_stream);
 int tomatis_plan_error_bits(tomatis_plan_t plan, uint32_t* bits, int32_t reset,
                             void* hip_stream);
@@ -274,9 +298,9 @@ int tomatis_plan_error_bits(tomatis_plan_t plan, uint32_t* bits, int32_t reset,
  *       in one workgroup per stream -- the small footprint to prefer when the
  *       call overlaps another stream group's transform.
  *   TOMATIS_OPT_LIMITER_ROUNDS (0 auto / 1 / 2): the fused limiter of
- *       standard-mode n_fft 2048 plans in two rounds (auto: on): round 1 leaves
- *       its output unscaled, round 2 scales it block by block inside its own
- *       frame loop, so only round 2's rescale is a tail.  Same results as 1. */
+ *       standard-mode n_fft 2048 plans in two rounds (auto: one round): round 1
+ *       leaves its output unscaled, round 2 scales it block by block inside its
+ *       own frame loop, so only round 2's rescale is a tail.  Same results. */
 #define TOMATIS_OPT_FUSE_LIMITER 1
 #define TOMATIS_OPT_LIMITER_SPIN 2
 #define TOMATIS_OPT_MINHOLD_SERIAL 3
@@ -292,7 +316,8 @@ int32_t tomatis_plan_limiter_rounds(tomatis_plan_t plan);
  * frame), FAST_LOOP (interior loop), RUN_FRAMES (frames per run, 0 auto),
  * RUN_ROUNDS, LEVELS_LEGACY, GATE_TF (transfer-function gate scan), MH_PARTS;
  * at launch: GATE_TF, ALPHA_SEQ (sequential xfade alpha), GAIN_LDS,
- * FUSE_LIMITER, WG (transform workgroup size).  Results are bit-identical
+ * FUSE_LIMITER, WG (transform workgroup size), FUSED_LEVELS; LIMITER_ROUNDS at
+ * plan creation.  Results are bit-identical
  * under every value (the decomposition tests vary them). */
 #define TOMATIS_DEV_FAST_LOOP 1
 #define TOMATIS_DEV_RUN_ROUNDS 2
@@ -306,6 +331,8 @@ int32_t tomatis_plan_limiter_rounds(tomatis_plan_t plan);
 #define TOMATIS_DEV_GAIN_LDS 10
 #define TOMATIS_DEV_FUSE_LIMITER 11
 #define TOMATIS_DEV_WG 12
+#define TOMATIS_DEV_LIMITER_ROUNDS 13  /* initial TOMATIS_OPT_LIMITER_ROUNDS of new plans */
+#define TOMATIS_DEV_FUSED_LEVELS 14    /* 0: tomatis_stft_ola_gated declines (host two-pass) */
 int tomatis_set_dev_option(int32_t key, int32_t value);
 
 /* max |x| over n floats as float bits (out zeroed by caller). */

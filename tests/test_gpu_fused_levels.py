@@ -1,0 +1,165 @@
+"""GPU: in-kernel levels + gate (tomatis_stft_ola_gated, DESIGN.md §5 "Fused
+levels") against the two-pass chain (tomatis_levels -> tomatis_gate_std ->
+tomatis_stft_ola_limited) and the oracle.
+
+The fused kernel computes every frame's r from the samples it loads for the FFT
+(the 16 128-sample leaves of numpy's pairwise sum, src/process_tomatis.py:373-376
+via dsp.frame_rms) and steps the gate automaton (:377-385) from the state a
+look-back pre-kernel found before its run; r, states, output and chunk peaks
+must equal the two-pass chain bit for bit.  A stream whose level hovers inside
+the hysteresis band for more than the look-back leaves runs unresolved: the
+pass is flagged (TOMATIS_ERR_GATE_CARRY) and re-run on the two-pass chain.
+"""
+import numpy as np
+import pytest
+
+from oracle import tomatis_oracle as orc
+from tomatis_audio_processor_amd.synth import synth_stream
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from tomatis_audio_processor_amd import engine
+    return torch, engine
+
+
+def _pair(E, ss, **kw):
+    """(gated pipe after run, two-pass y/r/states/peaks)"""
+    two = E.GatePipeline(ss, fused_levels=False, **kw)
+    two.run()
+    assert not two.gated_used
+    ref = (two.y.clone(), two.r.clone(), two.states.clone(), two.peaks.clone())
+    del two
+    pipe = E.GatePipeline(ss, **kw)
+    pipe.run()
+    return pipe, ref
+
+
+def _assert_same(torch, pipe, ref):
+    y, r, st, pk = ref
+    F = pipe.plan.total_frames
+    assert torch.equal(pipe.states[:F], st[:F]), "gate states differ"
+    assert torch.equal(pipe.r[:F].view(torch.int32), r[:F].view(torch.int32)), "r differs"
+    assert torch.equal(pipe.peaks, pk), "chunk peaks differ"
+    assert torch.equal(pipe.y, y), "output differs"
+
+
+@pytest.mark.parametrize("case", [
+    # (streams, seconds, ch, sr, hop, up_delay_ms, per-stream input gains)
+    ("c2_like", 1, 600, 2, 44100, 512, 250.0, [1.0]),
+    ("batch", 6, 45, 2, 48000, 512, 250.0, [1.0, 0.05, 0.3, 1.0, 0.15, 0.6]),
+    ("mono_hop256", 3, 40, 1, 44100, 256, 250.0, [1.0, 0.2, 0.02]),
+    ("no_delay", 2, 30, 2, 44100, 512, 0.0, [1.0, 0.1]),
+    ("long_delay", 1, 60, 2, 22050, 256, 2000.0, [0.7]),
+    ("short", 4, 1, 2, 44100, 512, 250.0, [1.0, 0.5, 0.1, 1.0]),
+])
+def test_gated_bit_identical(case):
+    torch, E = _engine()
+    _, ns, secs, ch, sr, hop, ud, gains = case
+    n = sr * secs + 391
+    ss = E.StreamSet.synthetic(ns, n, ch, sr, seed0=900)
+    for i, g in enumerate(gains):
+        if g != 1.0:
+            o = ss.offs[i]
+            ss.x[o:o + n * ch] *= g
+    pipe, ref = _pair(E, ss, gate_ui=50, n_fft=2048, hop=hop, up_delay_ms=ud)
+    assert pipe.gated_used, "an eligible standard-mode plan takes the fused gate"
+    assert pipe.gate_fallbacks == 0
+    _assert_same(torch, pipe, ref)
+
+
+def test_gated_ragged_and_two_rounds():
+    """Ragged stream lengths (edge runs, streams shorter than a frame) and the
+    two-round fused limiter under the fused gate."""
+    torch, E = _engine()
+    sr = 44100
+    xs = [synth_stream(31 + i, n, 2, sr) for i, n in
+          enumerate([sr * 70 + 13, 1500, sr * 3 + 1, 2048, sr * 41 + 999])]
+    ss = E.StreamSet.from_arrays(xs, sr)
+    pipe, ref = _pair(E, ss, gate_ui=50, n_fft=2048, hop=512)
+    assert pipe.gated_used
+    _assert_same(torch, pipe, ref)
+    pipe.plan.set_limiter_rounds(2)
+    pipe.run()
+    assert pipe.gated_used and pipe.gate_fallbacks == 0
+    _assert_same(torch, pipe, ref)
+
+
+def test_gated_vs_oracle():
+    torch, E = _engine()
+    sr, n = 44100, 44100 * 120 + 333
+    x = synth_stream(21, n, 2, sr)
+    ss = E.StreamSet.from_arrays([x], sr)
+    pipe = E.GatePipeline(ss, gate_ui=50, n_fft=2048, hop=512)
+    res = pipe.run()
+    assert pipe.gated_used
+    ref = orc.process_standard(x, sr, gate_ui=50, n_fft=2048, hop=512)
+    assert np.array_equal(res.stream_states(0), ref["states"])
+    assert np.array_equal(res.stream_r(0).view(np.uint32),
+                          np.asarray(ref["r"], np.float32).view(np.uint32))
+    y = res.output(0)
+    m = ref["wsum"][ref["pad"]:ref["pad"] + n] >= 1e-3
+    ok = np.ones(n, dtype=bool)
+    for (a, b), f in zip(res.chunk_ranges(0), res.scale_flags(0)):
+        if f:
+            ok[a:b] = False
+    err = float(np.max(np.abs(y[m & ok] - ref["y"][m & ok])))
+    assert err <= 1e-4, err
+
+
+def test_gated_fallback_hovering_level():
+    """A sine whose level sits at the gate threshold T (inside the +-1.5 dB
+    hysteresis band: neither "on" nor "off") for ~1400 frames: every run that
+    starts more than 512 frames after the stream's quiet first frame finds no
+    state-fixing frame in its look-back.  The pass must be flagged and re-run on
+    the two-pass chain, with the two-pass results; a loud stream in the same
+    batch is unaffected."""
+    torch, E = _engine()
+    sr, hop = 44100, 512
+    n = hop * 1400
+    T = -40.0  # gate_ui 50, log_percent
+    amp = np.sqrt(2.0) * 10.0 ** (T / 20.0)
+    t = np.arange(n) / sr
+    s = (amp * np.sin(2 * np.pi * 1000.0 * t)).astype(np.float32)
+    hover = np.stack([s, s], 1)
+    loud = synth_stream(8, n, 2, sr)
+    ss = E.StreamSet.from_arrays([hover, loud], sr)
+    pipe, ref = _pair(E, ss, gate_ui=50, n_fft=2048, hop=hop)
+    assert pipe.gate_fallbacks == 1, "the unresolved carry must re-run the pass"
+    assert not pipe.gated_used
+    _assert_same(torch, pipe, ref)
+    # the hovering stream stays in C1 after its quiet start (never D + 1 frames on)
+    st = pipe.result().stream_states(0)
+    assert (st == 1).all()
+    # next run: the plan tries the fused gate again (the flag is per pass)
+    pipe.run()
+    assert pipe.gate_fallbacks == 2
+    _assert_same(torch, pipe, ref)
+
+
+def test_gated_declines_other_shapes():
+    """Shapes outside the fused gate (n_fft 4096, hop 1024, xfade) run two passes."""
+    torch, E = _engine()
+    sr, n = 44100, 44100 * 20
+    ss = E.StreamSet.synthetic(1, n, 2, sr, seed0=5)
+    for kw in (dict(n_fft=4096, hop=1024), dict(n_fft=2048, hop=1024),
+               dict(n_fft=2048, hop=512, xfade_ms=500.0)):
+        pipe = E.GatePipeline(ss, gate_ui=50, **kw)
+        pipe.run()
+        assert not pipe.gated_used, kw
+
+
+def test_gated_full_size_c2():
+    """BASELINE C2 (60 min stereo 44.1 kHz, 2048/512): the bench's fused pass
+    equals the two-pass chain bit for bit."""
+    torch, E = _engine()
+    sr = 44100
+    n = 3600 * sr
+    ss = E.StreamSet.synthetic(1, n, 2, sr, seed0=1000)
+    pipe, ref = _pair(E, ss, gate_ui=50, n_fft=2048, hop=512)
+    assert pipe.gated_used and pipe.gate_fallbacks == 0
+    _assert_same(torch, pipe, ref)

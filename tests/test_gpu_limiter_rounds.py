@@ -40,6 +40,7 @@ def _scaled(E, torch, n_streams, n, ch, sr, gains, seed0):
 
 def _both(E, torch, ss, **kw):
     pipe = E.GatePipeline(ss, gate_ui=50, **kw)
+    pipe.plan.set_limiter_rounds(2)
     rounds = pipe.plan.limiter_rounds
     pipe.run()
     y2 = pipe.y.clone()
@@ -67,7 +68,7 @@ def test_two_rounds_bit_identical(case):
     n = sr * secs + 77
     ss = _scaled(E, torch, ns, n, ch, sr, gains, seed0=400)
     rounds, y2, pk2, pipe = _both(E, torch, ss, n_fft=n_fft, hop=hop)
-    assert rounds == 2, "an eligible standard-mode plan should take two rounds"
+    assert rounds == 2, "an eligible standard-mode plan takes two rounds when asked"
     assert torch.equal(pipe.peaks, pk2)
     assert torch.equal(pipe.y, y2), "two-round output differs from one round"
     # the limiter property on every stream: chunks over the limit end at it
@@ -86,6 +87,7 @@ def test_two_rounds_vs_oracle():
     x = synth_stream(21, n, 2, sr)
     ss = E.StreamSet.from_arrays([x], sr)
     pipe = E.GatePipeline(ss, gate_ui=50, n_fft=2048, hop=512)
+    pipe.plan.set_limiter_rounds(2)
     assert pipe.plan.limiter_rounds == 2
     res = pipe.run()
     assert pipe.plan.error_bits() == 0
@@ -109,6 +111,7 @@ def test_two_rounds_fault_recovery():
     sr, n = 44100, 44100 * 120 + 5
     ss = E.StreamSet.synthetic(1, n, 2, sr, seed0=77)
     pipe = E.GatePipeline(ss, gate_ui=50, n_fft=2048, hop=512)
+    pipe.plan.set_limiter_rounds(2)
     assert pipe.plan.limiter_rounds == 2
     pipe.run()
     y0 = pipe.y.clone()
@@ -123,8 +126,9 @@ def test_two_rounds_fault_recovery():
 
 def test_two_rounds_timeshard_edges():
     """Time shards leave their edge chunks to the peak exchange: the round-2
-    plan stops at them and the tails skip them.  Shards (two rounds each) vs
-    the unsharded stream in one round: bit-identical."""
+    plan stops at them and the tails skip them.  Shards (two rounds each, a
+    process-wide dev override) vs the unsharded stream in one round:
+    bit-identical."""
     torch, E = _engine()
     from tomatis_audio_processor_amd import timeshard as TS
     sr, n = 44100, 44100 * 240 + 11
@@ -133,7 +137,9 @@ def test_two_rounds_timeshard_edges():
     pipe = E.GatePipeline(E.StreamSet.from_arrays([x], sr), **params)
     pipe.plan.set_limiter_rounds(1)
     res = pipe.run()
-    y, st, pk = TS.run_emulated(x, sr, 3, **params)
+    from tomatis_audio_processor_amd._lib import dev_options
+    with dev_options(LIMITER_ROUNDS=2):
+        y, st, pk = TS.run_emulated(x, sr, 3, **params)
     assert np.array_equal(st, res.stream_states(0))
     assert pk.tobytes() == res.stream_peaks(0).tobytes()
     assert y.tobytes() == res.output(0).tobytes()

@@ -19,13 +19,16 @@ GATE_SEGMENT = 1024      # TOMATIS_GATE_SEGMENT
 GATE_NONE = -536870912   # TOMATIS_GATE_NONE
 ERR_LIMITER_WAIT = 1     # TOMATIS_ERR_LIMITER_WAIT
 ERR_PAIR_BARRIER = 2     # TOMATIS_ERR_PAIR_BARRIER
+ERR_GATE_CARRY = 4       # TOMATIS_ERR_GATE_CARRY
+E_UNSUPPORTED = -2       # TOMATIS_E_UNSUPPORTED
 OPT_FUSE_LIMITER = 1     # TOMATIS_OPT_FUSE_LIMITER
 OPT_LIMITER_SPIN = 2     # TOMATIS_OPT_LIMITER_SPIN
 OPT_MINHOLD_SERIAL = 3   # TOMATIS_OPT_MINHOLD_SERIAL
 OPT_LIMITER_ROUNDS = 4   # TOMATIS_OPT_LIMITER_ROUNDS
 # development overrides (TOMATIS_DEV_*: tests and A/B experiments only)
 DEV_KEYS = dict(FAST_LOOP=1, RUN_ROUNDS=2, RUN_FRAMES=3, LEVELS_LEGACY=4, GATE_TF=5, MH_PARTS=6,
-                FORCE_LDS=7, P64=8, ALPHA_SEQ=9, GAIN_LDS=10, FUSE_LIMITER=11, WG=12)
+                FORCE_LDS=7, P64=8, ALPHA_SEQ=9, GAIN_LDS=10, FUSE_LIMITER=11, WG=12,
+                LIMITER_ROUNDS=13, FUSED_LEVELS=14)
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 F32, F64 = 0, 1
@@ -96,6 +99,7 @@ _SIGS = {
     "tomatis_stft_ola_limited_edges": (C.c_int, [_P, _P, _P, C.c_int32, _P, _P, _P, C.c_float,
                                                  C.c_int32, _P]),
     "tomatis_apply_limiter_edges": (C.c_int, [_P, _P, _P, C.c_float, C.c_int32, _P]),
+    "tomatis_stft_ola_gated": (C.c_int, [_P, _P, _P, C.c_int32, _P, _P, C.c_float, _P, _P, _P]),
     "tomatis_ts_summary": (C.c_int, [_P, _P, C.c_int32, C.c_int32, _P, _P]),
     "tomatis_ts_gate": (C.c_int, [_P, _P, _P, C.c_int32, C.c_int32, _P, _P, _P]),
     "tomatis_plan_error": (C.c_int, [_P, _P]),

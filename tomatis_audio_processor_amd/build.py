@@ -30,7 +30,7 @@ UNITS = {  # source -> extra flags
     "tm_analysis.hip": [],
 }
 DEPS = [os.path.join(CSRC, f) for f in (*UNITS, "tm_common.h", "tm_fft.h", "tm_shared.h",
-                                        "tm_lds_fft.h", "tm_host_dsp.h")] + \
+                                        "tm_lds_fft.h", "tm_host_dsp.h", "tm_gate.h")] + \
        [os.path.join(ROOT, "include", "tomatis_hip.h"), os.path.abspath(__file__)]
 OUT = os.path.join(HERE, "libtomatis_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

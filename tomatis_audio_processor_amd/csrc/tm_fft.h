@@ -102,8 +102,14 @@ __device__ __forceinline__ void xsync(cf* buf = nullptr, uint32_t* err = nullptr
   }
 }
 
-// exchange-2 column of element (a, c) in a row
-__device__ __forceinline__ int x2col(int a, int c) { return 8 * c + (a ^ (c & 7)); }
+// exchange-2 column of element (a, c) in a row: XOR swizzle a ^ g(c) with
+// g(c) = (c & 7) ^ ((c >> 2) & 2).  For P = 64 (c < 8) g(c) = c; for P = 128
+// (c < 16) plain c & 7 maps c and c + 8 onto the same banks (2-way conflicts
+// on the exchange-2 reads, 16.5 % of LDS cycles measured on C5x); folding c's
+// bit 3 into bit 1 makes exchanges 2 and 3 conflict-free for both (checked
+// against the gfx950 lane-group / bank rules of every exchange instruction,
+// MI355X_MICROARCH.md "LDS")
+__device__ __forceinline__ int x2col(int a, int c) { return 8 * c + (a ^ ((c & 7) ^ ((c >> 2) & 2))); }
 
 // forward FFT.  v: 32 registers (input x[L + P*n2]); out: bin layout above.
 // twN: LDS W_N^{n1*k2} in lane-pair layout [k2/2][n1][k2&1] (16-B aligned);

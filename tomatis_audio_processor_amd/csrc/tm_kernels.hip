@@ -25,10 +25,12 @@
 #include "tm_host_dsp.h"
 #include "tm_fft.h"
 #include "tm_shared.h"
+#include "tm_gate.h"
 #include "../../include/tomatis_hip.h"
 
 using namespace tdsp;
 using namespace tshared;
+using namespace tgate;
 
 namespace {
 
@@ -336,27 +338,6 @@ __global__ __launch_bounds__(256) void k_frame_r(const TomatisStream* __restrict
 // Standard gate (process_tomatis.py:373-385) as a transfer-function scan.
 // state id: 0 = C1 idle, 1..D = C1 pending for (id-1) frames, D+1 = C2.
 // ===========================================================================
-__device__ __forceinline__ bool in_exc(uint32_t b, const uint32_t* e, int n) {
-  bool hit = false;
-  for (int i = 0; i < n; ++i) hit |= (b == e[i]);
-  return hit;
-}
-__device__ __forceinline__ uint8_t gate_pred(float r, const TomatisStream& S) {
-  const uint32_t b = __float_as_uint(r);
-  if (r != r) return 0;
-  const bool on = (b >= S.on_bits) != in_exc(b, S.on_exc, S.n_on_exc);
-  const bool off = (b <= S.off_bits) != in_exc(b, S.off_exc, S.n_off_exc);
-  return (uint8_t)((on ? 1 : 0) | (off ? 2 : 0));
-}
-__device__ __forceinline__ int gate_step(int id, uint8_t pr, int D) {
-  if (id == D + 1) return (pr & 2) ? 0 : id;
-  if (pr & 1) {
-    const int age = (id == 0) ? 0 : id;  // frames since pending was set, after this frame
-    return (age >= D) ? D + 1 : age + 1;
-  }
-  return 0;
-}
-
 __global__ __launch_bounds__(256) void k_gate_tf(const float* __restrict__ r,
                                                  const TomatisStream* __restrict__ st,
                                                  const GateSeg* __restrict__ segs, int nseg,
@@ -1593,6 +1574,10 @@ struct tomatis_plan_s {
   uint32_t* chunk_final = nullptr;
   uint32_t* pieces = nullptr;
   int max_pieces = 0;
+  // in-kernel levels + gate (tomatis_stft_ola_gated): per-run carry-in
+  int32_t* gate_carry = nullptr;
+  float* gate_win = nullptr;
+  int gate_cap = 0;
   // run-scan gate (exclusive on/off predicates)
   bool gate_excl = false;
   void* gsum = nullptr;
@@ -1648,8 +1633,8 @@ int launch_check() { return hipfail(hipGetLastError()); }
 
 namespace tshared {
 // development overrides (tomatis_set_dev_option); -1 = the default
-constexpr int kDevKeys = 13;
-static int g_dev[kDevKeys] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+constexpr int kDevKeys = 15;
+static int g_dev[kDevKeys] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 int dev_opt(int key, int dflt) {
   const int v = (key > 0 && key < kDevKeys) ? g_dev[key] : -1;
   return v < 0 ? dflt : v;
@@ -1679,7 +1664,7 @@ int tomatis_plan_destroy(tomatis_plan_t p) {
                   p->grp_base, p->leaf_base, p->leaves, p->gsum, p->gcarry, p->gcarry_in,
                   p->aq, p->afin, p->acin,
                   p->chunk_need, p->chunk_done, p->chunk_rng, p->err, p->twL,
-                  p->partner, p->chunk_final, p->pieces,
+                  p->partner, p->chunk_final, p->pieces, p->gate_carry, p->gate_win,
                   p->pw_leaf, p->pw_prog, p->blue_b, p->blue_h, p->glb_work};
   for (void* q : ptrs) dfree(q);
   delete p;
@@ -1716,9 +1701,11 @@ static int build_runs(tomatis_plan_s* p) {
   const int ns = p->n_streams;
   int rc;
   // two-round fused limiter: standard-mode register plans (two gain rows, LDS),
-  // n_fft 2048 (the interior loop); TOMATIS_OPT_LIMITER_ROUNDS 1 turns it off
+  // n_fft 2048 (the interior loop), when TOMATIS_OPT_LIMITER_ROUNDS asks for it
+  // (auto = one round: measured on C2, round 2's in-loop rescale hides 0.15 ms
+  // of tail but the split costs about as much -- DESIGN.md §6)
   const bool two = !p->generic && P == 64 && d.alpha_mode == 0 && p->total_chunks > 0 &&
-                   p->lim_rounds != 1 && N <= 2048;
+                   p->lim_rounds == 2 && N <= 2048;
   const int64_t tf_total = std::max<int64_t>(1, p->total_frames);
   // Runs.  Per stream, the emitted frames [e_lo, e_hi) whose run can take the
   // fused kernel's interior loop (full frame loads back to the warm-up frames,
@@ -2187,6 +2174,7 @@ int tomatis_plan_create(tomatis_plan_t* out, const TomatisPlanDesc* desc, const 
   if (!p) return TOMATIS_E_NOMEM;
   p->d = d;
   p->n_streams = n_streams;
+  p->lim_rounds = std::max(0, std::min(2, dev_opt(TOMATIS_DEV_LIMITER_ROUNDS, 0)));
   const int N = d.n_fft, hop = d.hop;
   // (lanes P, registers NR) per transform: 2048 = 128 x 16, 4096 = 128 x 32
   // n_fft 2048: one wave per frame (P = 64, 32 registers, wave-local exchanges)
@@ -2509,10 +2497,16 @@ int tomatis_minhold_bisect(tomatis_plan_t p, const double* levels, const double*
   return launch_check();
 }
 
+// in-kernel levels + gate outputs (tomatis_stft_ola_gated)
+struct GateOut {
+  float* r;
+  uint8_t* states;
+};
+
 static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, int32_t n_rows,
                          const uint16_t* rows, float* y, uint32_t* peaks, float limit,
-                         void* hs) {
-  if (!p || !x || !gains || !rows || !y || !peaks || n_rows < 1) return TOMATIS_E_ARG;
+                         void* hs, const GateOut* gate = nullptr) {
+  if (!p || !x || !gains || (!rows && !gate) || !y || !peaks || n_rows < 1) return TOMATIS_E_ARG;
   if (p->n_runs == 0) return TOMATIS_OK;
   hipStream_t s = (hipStream_t)hs;
   const int N = p->d.n_fft;
@@ -2609,6 +2603,35 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
   A.partner = nullptr;
   A.pieces = nullptr;
   A.max_pieces = 0;
+  A.gated = 0;
+  A.gate_D = p->d.up_delay_frames;
+  A.r_out = nullptr;
+  A.st_out = nullptr;
+  A.gcarry = nullptr;
+  A.gwin = nullptr;
+  if (gate) {
+    // per run: the carry-in state id and leaf window (k_gate_carry), then the
+    // transform computes every frame's r and state from the input it loads
+    if (p->n_runs > p->gate_cap) {
+      dfree(p->gate_carry);
+      dfree(p->gate_win);
+      p->gate_carry = nullptr;
+      p->gate_win = nullptr;
+      p->gate_cap = 0;
+      if (hipMalloc(reinterpret_cast<void**>(&p->gate_carry), (size_t)p->n_runs * sizeof(int32_t)) ||
+          hipMalloc(reinterpret_cast<void**>(&p->gate_win), (size_t)p->n_runs * 16 * sizeof(float)))
+        return TOMATIS_E_NOMEM;
+      p->gate_cap = p->n_runs;
+    }
+    A.gated = 1;
+    A.r_out = gate->r;
+    A.st_out = gate->states;
+    A.gcarry = p->gate_carry;
+    A.gwin = p->gate_win;
+    launch_gate_carry(A, p->P, p->SH, p->d.ch, p->gate_carry, p->gate_win, s);
+    const int rc = launch_check();
+    if (rc) return rc;
+  }
   if (limit > 0.f) {
     if (!p->chunk_done) return TOMATIS_E_UNSUPPORTED;
     if (hipMemsetAsync(p->chunk_done, 0, (size_t)p->total_chunks * 4, s)) return TOMATIS_E_HIP;
@@ -2710,6 +2733,38 @@ int tomatis_stft_ola_limited_edges(tomatis_plan_t p, const float* x, const float
     if (!rc) rc = limiter_launch(p, y, peaks, limit, edge_mask ? 1 : 0, edge_mask, hs);
   }
   p->edge_mask = 0;
+  return rc;
+}
+
+// tomatis_stft_ola_gated eligibility: the fused kernel's interior loop at
+// n_fft 2048 with hop 256 / 512 (the 16-leaf window spans whole hop blocks),
+// the standard gate (two rows), float input used as is, and every stream
+// addressable by the 31-bit buffer offsets of k_gate_carry's loads
+static bool gated_eligible(const tomatis_plan_s* p) {
+  const TomatisPlanDesc& d = p->d;
+  if (dev_opt(TOMATIS_DEV_FUSED_LEVELS, 1) == 0) return false;
+  if (p->generic || p->lds || p->P != 64 || p->NR != 32 || d.n_fft != 2048) return false;
+  if (!(p->SH == 4 || p->SH == 8) || d.ch < 1 || d.ch > 2 || d.alpha_mode != 0) return false;
+  for (int s = 0; s < p->n_streams; ++s) {
+    const TomatisStream& S = p->hs[s];
+    if (S.in_scale != 1.f || S.n * d.ch * 4 > 0x7fffffffll) return false;
+  }
+  return true;
+}
+
+int tomatis_stft_ola_gated(tomatis_plan_t p, const float* x, const float* gains, int32_t n_rows,
+                           float* y, uint32_t* peaks, float limit, float* r_out,
+                           uint8_t* states_out, void* hs) {
+  if (!p || !x || !gains || !y || !peaks || !r_out || !states_out || n_rows != 2 || limit < 0.f)
+    return TOMATIS_E_ARG;
+  if (!gated_eligible(p)) return TOMATIS_E_UNSUPPORTED;
+  const GateOut g{r_out, states_out};
+  if (!(limit > 0.f)) return stft_ola_impl(p, x, gains, n_rows, nullptr, y, peaks, 0.f, hs, &g);
+  const bool fuse = p->chunk_done && p->fuse_span > 0 && p->fuse_enabled &&
+                    p->fuse_span <= fuse_max_span(p) && dev_opt(TOMATIS_DEV_FUSE_LIMITER, 1) != 0;
+  if (fuse) return stft_ola_impl(p, x, gains, n_rows, nullptr, y, peaks, limit, hs, &g);
+  int rc = stft_ola_impl(p, x, gains, n_rows, nullptr, y, peaks, 0.f, hs, &g);
+  if (!rc) rc = limiter_launch(p, y, peaks, limit, 0, 0, hs);
   return rc;
 }
 

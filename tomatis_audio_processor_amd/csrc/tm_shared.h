@@ -69,9 +69,24 @@ struct MainArgs {
   // left to the tail}, then count x {partner block, scale bits}
   const uint32_t* pieces;
   int max_pieces;
+  // in-kernel levels + gate (tomatis_stft_ola_gated, DESIGN.md §5 "Fused
+  // levels"): every frame's r (numpy pairwise order) and gate state are computed
+  // from the input the transform loads and written here; each run starts from
+  // k_gate_carry's carry-in state id and 16-leaf window
+  int gated;
+  int gate_D;           // up-delay frames
+  float* r_out;
+  uint8_t* st_out;
+  const int32_t* gcarry;  // per run: state id before its first frame (< 0: unresolved)
+  const float* gwin;      // per run: the 16 leaf sums of the frame before its first
 };
 void launch_r2_plan(const MainArgs& A, const uint32_t* chunk_final, uint32_t* pieces,
                     hipStream_t s);
+// k_gate_carry over every run of A (A.run_base = 0): carry-in state id and leaf
+// window per run; H_max frames of look-back before a run is left unresolved
+void launch_gate_carry(const MainArgs& A, int P, int SH, int ch, int32_t* gcarry, float* gwin,
+                       hipStream_t s);
+constexpr int kGateLookback = 512;
 
 // Any-size path (any n_fft in [2, kMaxNfft], any hop, 1..kMaxCh channels): per
 // (frame, channel pair) a Stockham FFT of length M (n_fft when it is a power

@@ -19,9 +19,11 @@
 #include "tm_fft.h"
 #include "tm_lds_fft.h"
 #include "tm_shared.h"
+#include "tm_gate.h"
 
 using namespace tdsp;
 using namespace tshared;
+using namespace tgate;
 
 #ifndef TM_DEV_WG
 #define TM_DEV_WG 256
@@ -178,6 +180,101 @@ __device__ __forceinline__ float bloadf(__amdgpu_buffer_rsrc_t r, int voff, int 
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
 }
 
+// ---------------------------------------------------------------------------
+// In-kernel levels (n_fft 2048, hop 256 / 512; src/process_tomatis.py:43-52,
+// 369-371).  numpy's frame r is a perfect binary tree over the frame's 16
+// leaves of 128 samples (pairwise_sum), and each leaf is 8 sequential chains
+// (samples c, c+8, ..., c+120) combined as ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7));
+// a hop block is LB = hop/128 whole leaves shared by every frame covering it,
+// so each frame adds the leaves of its newest block only.  The block (lane L,
+// register j = sample L + 64 j) goes through LDS into chain order (conflict-free
+// layout: chain stride 20, leaf stride 160 floats), each chain is summed in
+// order by one lane, the 8 chains reduce by DPP, and the frame's 16 leaf sums
+// sit in lanes 0..15 of one VGPR (the "window").  Every operation is a plain
+// IEEE float32 op in numpy's order (no contraction: bit-identical to k_leaves).
+// ---------------------------------------------------------------------------
+constexpr int kLvCS = 20, kLvLS = 160;
+
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, true));
+}
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141;
+template <int N> constexpr int kDppRowShl = 0x100 + N;
+template <int N> constexpr int kDppRowShr = 0x110 + N;
+
+// m*m of one sample, m = sqrt(mean over channels of x^2) (CH = 2: L + iR).
+// This unit compiles with -ffp-contract=fast, which lets the backend fuse any
+// multiply-add whatever the source pragmas: the squares go through opaque
+// copies so L^2 + R^2 stays two roundings, as numpy's frame**2 then sum.
+template <int CH>
+__device__ __forceinline__ float lv_msq(cf v) {
+  if constexpr (CH == 2) {
+    const float ll = opaque_f(v.x * v.x), rr = opaque_f(v.y * v.y);
+    const float m = sqrtf((ll + rr) * 0.5f);
+    return m * m;
+  } else {
+    const float m = sqrtf(v.x * v.x);
+    return m * m;
+  }
+}
+
+// leaf sums of the hop block in the last SH registers of v; returns them in
+// lanes 8 l (l < LB).  scr: this sequence's LDS scratch (>= LB * kLvLS floats)
+template <int CH, int SH, int NRV>
+__device__ __forceinline__ float lv_leaves(const cf (&v)[NRV], float* scr, int L) {
+  constexpr int LB = SH / 2;
+#pragma unroll
+  for (int j = 0; j < SH; ++j)
+    scr[(j >> 1) * kLvLS + (L & 7) * kLvCS + (L >> 3) + 8 * (j & 1)] = lv_msq<CH>(v[NRV - SH + j]);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int leaf = min(L >> 3, LB - 1);
+  const float4* p = reinterpret_cast<const float4*>(scr + leaf * kLvLS + (L & 7) * kLvCS);
+  const float4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+  float a = q0.x;
+  a = a + q0.y; a = a + q0.z; a = a + q0.w;
+  a = a + q1.x; a = a + q1.y; a = a + q1.z; a = a + q1.w;
+  a = a + q2.x; a = a + q2.y; a = a + q2.z; a = a + q2.w;
+  a = a + q3.x; a = a + q3.y; a = a + q3.z; a = a + q3.w;
+  a = a + dpp<kDppXor1>(a);        // lanes c, c^1: r0 + r1 ...
+  a = a + dpp<kDppXor2>(a);        // (r0 + r1) + (r2 + r3) in lanes 0..3
+  a = a + dpp<kDppHalfMirror>(a);  // lane 0: + ((r4 + r5) + (r6 + r7)) from lane 7
+  // the scratch is reused by the next block / the FFT exchanges: reads done
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return a;
+}
+
+// window of the next frame: drop the oldest block's LB leaves, append the new
+// block's (lanes 16 - LB + l <- lane 8 l); FWD false: the previous frame
+// (backward scan), prepend at lanes 0..LB-1 and drop the newest
+template <int SH, bool FWD>
+__device__ __forceinline__ float lv_window(float lw, float nl) {
+  constexpr int LB = SH / 2;
+  lw = FWD ? dpp<kDppRowShl<LB>>(lw) : dpp<kDppRowShr<LB>>(lw);
+#pragma unroll
+  for (int l = 0; l < LB; ++l) {
+    const int v = __builtin_amdgcn_readlane(__float_as_int(nl), 8 * l);
+    __asm__("v_writelane_b32 %0, %1, %2" : "+v"(lw) : "s"(v), "n"(FWD ? 16 - LB + l : l));
+  }
+  return lw;
+}
+
+// frame r from the window: perfect tree over lanes 0..15, mean, + EPS, sqrt
+// (k_frame_r's order); wave-uniform
+__device__ __forceinline__ float lv_frame_r(float lw) {
+  float t = lw + dpp<kDppRowShl<1>>(lw);
+  t = t + dpp<kDppRowShl<2>>(t);
+  t = t + dpp<kDppRowShl<4>>(t);
+  t = t + dpp<kDppRowShl<8>>(t);
+  const float tot = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(t)));
+  const float mean = tot * (1.0f / 2048.0f);  // exact (numpy divides by n = 2^11)
+  return sqrtf(opaque_f(mean) + kEps32);
+}
+
 // read-only (for the kernel's lifetime) data through the scalar cache: a
 // constant-address-space view makes uniform loads s_load (lgkmcnt-counted)
 typedef __attribute__((address_space(4))) const uint32_t cu32;
@@ -192,7 +289,10 @@ typedef __attribute__((address_space(4))) const uint32_t cu32;
 // cross-fade lattice rows from global (row is wave-uniform, so is the branch).
 // PR: round 2 of the two-round fused limiter (MainArgs::partner): each interior
 // run also rescales its round-1 partner's output inside its frame loop.
-template <int P, int NR, int SH, int CH, int GM, bool PF, bool NT, int WG, bool PR = false>
+// GT: in-kernel levels + gate (MainArgs::gated): each frame's r and state come
+// from the frame the kernel has loaded (no separate level pass, no row ids).
+template <int P, int NR, int SH, int CH, int GM, bool PF, bool NT, int WG, bool PR = false,
+          bool GT = false>
 __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(MainArgs A) {
 #ifdef TM_PROFILE
   const unsigned long long t_k0 = __builtin_amdgcn_s_memtime();
@@ -268,6 +368,48 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   const int64_t out_end = S.out_begin + S.out_len;
   const float oscale = S.out_scale;
   const float iscale = S.in_scale;
+
+  // ---- in-kernel gate: carry-in state and leaf window from k_gate_carry ----
+  static_assert(!GT || (P == 64 && NR == 32 && (SH == 4 || SH == 8)),
+                "in-kernel levels: n_fft 2048, hop 256 / 512");
+  constexpr int NBLK = NR / SH;  // hop blocks per frame
+  float lw = 0.f;                // lanes 0..15: the current frame's leaf sums
+  int gid = 0;                   // gate state id (tm_gate.h)
+  if constexpr (GT) {
+    lw = (L < 16) ? A.gwin[(int64_t)run_id * 16 + L] : 0.f;
+    gid = __builtin_amdgcn_readfirstlane(A.gcarry[run_id]);
+    if (gid < 0) {  // look-back did not resolve: the host re-runs the two-pass path
+      if (L == 0) atomicOr(A.err, TOMATIS_ERR_GATE_CARRY);
+      gid = 0;
+    }
+  }
+  float* const lscr = reinterpret_cast<float*>(buf);  // leaf scratch (free at the frame top)
+  // predicate thresholds in SGPRs; the exception lists (numpy log10's
+  // non-monotone steps, rarely non-empty) are read from the stream table only
+  // when present, so the frame loop does not hold 10 more SGPRs
+  const uint32_t g_on = S.on_bits, g_off = S.off_bits;
+  const bool g_exc = (S.n_on_exc | S.n_off_exc) != 0;
+  // frame k: leaves of its newest block (the last SH registers of fr), r,
+  // predicate, state; r and state of emitted frames stored by lane 0
+  auto gate_frame = [&](const cf (&fr)[NR], int64_t k, bool emit) -> uint32_t {
+    lw = lv_window<SH, true>(lw, lv_leaves<CH, SH, NR>(fr, lscr, L));
+    const float r = lv_frame_r(lw);
+    uint8_t pr;
+    if (g_exc) {
+      pr = gate_pred(r, A.st[opaque(R.s)]);
+    } else {
+      const uint32_t b = __float_as_uint(r);
+      pr = (r != r) ? 0 : (uint8_t)((b >= g_on ? 1 : 0) | (b <= g_off ? 2 : 0));
+    }
+    gid = gate_step(gid, pr, A.gate_D);
+    const bool c2 = gid == A.gate_D + 1;
+    if (emit && L == 0) {
+      const int64_t fo = S.frame_base + k;
+      A.r_out[fo] = r;
+      A.st_out[fo] = (uint8_t)(c2 ? 2 : 1);
+    }
+    return c2 ? 1u : 0u;
+  };
 
   if (valid && R.ka == 0 && S.first_start > S.out_begin) {  // adaptive: zeros before frame 0
     for (int64_t p = S.out_begin + L; p < min(S.first_start, out_end); p += P)
@@ -459,7 +601,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
         yP = A.y + (int64_t)(((uint64_t)hi << 32) | lo);
       }
     }
-    uint32_t rw_nx = row_word(0);
+    uint32_t rw_nx = GT ? 0u : row_word(0);  // (GT: no row ids)
     {  // frame 0, null stores (the loop's issue pattern), new hop of frame 1
       ld_old(0, v);
       cf t[SH];
@@ -472,9 +614,14 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       ld_new(min(1, nit - 1), nh);
     }
     for (int it = 0; it < nit; ++it) {
-      const uint32_t row = row_of(rw_nx, it);
-      rw_nx = row_word(min(it + 1, nit - 1));
       const bool emit = it >= nwarm;
+      uint32_t row;
+      if constexpr (GT) {
+        row = gate_frame(v, kfirst + it, emit);
+      } else {
+        row = row_of(rw_nx, it);
+        rw_nx = row_word(min(it + 1, nit - 1));
+      }
       if constexpr (PR) {
         // piece it of the partner -> LDS slot (branch-free: past the list the
         // resource is empty, the load returns zeros and the store drops)
@@ -543,6 +690,13 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
           const f32x4 b = {__float_as_uint(t.x), __float_as_uint(t.y), __float_as_uint(t.z),
                            __float_as_uint(t.w)};
           __builtin_amdgcn_raw_buffer_store_b128(b, rps, L * 16, u * 1024, 2);
+          // a 16-byte store reads its data VGPRs after issue: one wait state
+          // before any VALU write of them (hipcc scheduled the next piece's
+          // product into the same registers directly behind the store, and the
+          // store wrote the new value for the last lanes; tools/store_hazard.py)
+          __builtin_amdgcn_sched_barrier(0);
+          __asm__ volatile("s_nop 0");
+          __builtin_amdgcn_sched_barrier(0);
         }
       }
       TPROF(6, acc[0].x);
@@ -585,15 +739,18 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       return A.rows[S.frame_base + min(kk, kmax)];
     };
     cf nx[NR];
-    uint32_t row_nx = load_row(kfirst);
+    uint32_t row_nx = GT ? 0u : load_row(kfirst);  // (GT: no row ids)
     if constexpr (PF) load_frame(kfirst, nx);
 
     for (int it = 0; it < nit; ++it) {
       const int64_t k = kfirst + it;
       const bool live = valid && (k < R.kb);
       const int64_t s_k = S.first_start + k * HOP;
-      const uint32_t row = __builtin_amdgcn_readfirstlane(live ? row_nx : 0u);
-      row_nx = load_row(k + 1);
+      uint32_t row = 0;
+      if constexpr (!GT) {
+        row = __builtin_amdgcn_readfirstlane(live ? row_nx : 0u);
+        row_nx = load_row(k + 1);
+      }
       cf v[NR];
       if constexpr (PF) {
   #pragma unroll
@@ -602,6 +759,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       } else {
         load_frame(k, v);
       }
+      if constexpr (GT) row = gate_frame(v, k, live && k >= R.ka);
       transform(v, row);
       if (live && k >= R.ka) {
         if (k == next_chunk_k) {
@@ -768,6 +926,100 @@ __global__ __launch_bounds__(64) void k_r2_plan(MainArgs A, const uint32_t* __re
     o[0] = (uint32_t)n;
     o[1] = (uint32_t)stop;
   }
+}
+
+// In-kernel gate, part 1 (tomatis_stft_ola_gated): per run, the gate state
+// before its first frame kf = max(0, ka - rmax + 1) and the 16-leaf window of
+// frame kf - 1, which the fused kernel continues frame by frame.  The gate
+// automaton forgets its past at an anchor frame: a frame that is not "on" and
+// "off" leaves C1 idle whatever came before, and D + 1 consecutive frames "on"
+// and not "off" leave C2 (every pending count matures, C2 stays).  One wave
+// per run walks back from kf - 1 computing frame levels exactly as the fused
+// kernel (the same leaf / window / tree code, blocks read from HBM, zeros
+// outside the stream) until the nearest anchor, frame 0 (the automaton starts
+// C1 idle, src/process_tomatis.py:288-289) or kGateLookback frames (then the
+// run is left unresolved, carry = -1, and the host falls back to the two-pass
+// path); the state then runs forward over the recorded predicates to kf.
+// Blocks are prefetched 4 ahead.
+template <int CH, int SH>
+__global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restrict__ carry,
+                                                   float* __restrict__ win) {
+  constexpr int P = 64, NR = 32, HOP = SH * P, NB = NR / SH, LB = SH / 2, PFD = 4;
+  __shared__ __attribute__((aligned(16))) float scr[LB * kLvLS];
+  __shared__ uint8_t prs[kGateLookback];
+  const int run = blockIdx.x;
+  if (run >= A.n_runs) return;
+  const int L = threadIdx.x;
+  const Run R = A.runs[run];
+  const TomatisStream S = A.st[R.s];
+  const int D = A.gate_D;
+  const int64_t kf = max<int64_t>(0, R.ka - (A.rmax - 1));
+  const __amdgpu_buffer_rsrc_t rx =
+      mk_rsrc(A.x + S.in_off, (uint32_t)min<int64_t>(S.n * CH * 4, 0x7fffffffll));
+  auto load_block = [&](int64_t b, cf (&dst)[SH]) {  // block b of the frame grid
+    const int64_t p0 = S.first_start + b * HOP + L;
+#pragma unroll
+    for (int j = 0; j < SH; ++j)  // negative / past-the-end positions: out of range -> 0
+      dst[j] = bload<CH>(rx, (int)(uint32_t)((p0 + 64 * j) * (CH * 4)), 0);
+  };
+  // window of frame kf - 1: blocks kf - 1 .. kf + NB - 2
+  float lw = 0.f;
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    cf b[SH];
+    load_block(kf - 1 + i, b);
+    lw = lv_window<SH, true>(lw, lv_leaves<CH, SH, SH>(b, scr, L));
+  }
+  if (L < 16) win[(int64_t)run * 16 + L] = lw;
+  int id = 0;
+  if (kf > 0) {
+    int64_t j = kf - 1;          // the window holds frame j
+    int64_t a_k = -2;            // anchor: the state after frame a_k is a_id (-2: none)
+    int a_id = 0, on_run = 0, n = 0;
+    cf bq[PFD][SH];              // blocks j - 1 - u, prefetched
+    sfor<0, PFD>([&](auto uu) { load_block(j - 1 - decltype(uu)::value, bq[decltype(uu)::value]); });
+    bool more = true;
+    while (more) {
+      sfor<0, PFD>([&](auto uu) {
+        constexpr int u = decltype(uu)::value;
+        if (more) {
+          const uint8_t pr = gate_pred(lv_frame_r(lw), S);
+          if (L == 0) prs[n] = pr;
+          ++n;
+          on_run = ((pr & 1) && !(pr & 2)) ? on_run + 1 : 0;
+          if (!(pr & 1) && (pr & 2)) {
+            a_k = j;  // sync: C1 idle after j
+            a_id = 0;
+            more = false;
+          } else if (on_run == D + 1) {
+            a_k = j + D;  // D + 1 frames on: C2 after j + D
+            a_id = D + 1;
+            more = false;
+          } else if (j == 0) {
+            a_k = -1;  // stream start: C1 idle before frame 0
+            a_id = 0;
+            more = false;
+          } else if (n >= kGateLookback) {
+            more = false;  // unresolved
+          } else {
+            lw = lv_window<SH, false>(lw, lv_leaves<CH, SH, SH>(bq[u], scr, L));
+            load_block(j - 1 - PFD, bq[u]);
+            --j;
+          }
+        }
+      });
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (a_k == -2) {
+      id = -1;
+    } else {
+      id = a_id;
+      for (int64_t k = a_k + 1; k < kf; ++k) id = gate_step(id, prs[kf - 1 - k], D);
+    }
+  }
+  if (L == 0) carry[run] = id;
 }
 
 // Generic hop: same transform, windowed frame outputs to scratch, then a gather.
@@ -1105,6 +1357,23 @@ void launch_main_pf(const MainArgs& A, int ch, hipStream_t s) {
   constexpr bool kNoLdsGains = P == 128 && NR == 32;
   const int gm = kNoLdsGains ? 0 : (A.n_rows_lds > 0 ? (A.lds_mixed ? 2 : 1) : 0);
   const dim3 g((A.n_runs + WG / P - 1) / (WG / P)), b(WG);
+  if constexpr (P == 64 && (SH == 4 || SH == 8)) {
+    if (A.gated) {  // in-kernel levels + gate (two-row tables: gm == 1, host-checked)
+      if (A.partner) {
+        if constexpr (WG == 512) {
+          if (ch == 2)
+            hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 1, PF, NT, WG, true, true>), g, b, 0, s, A);
+          else
+            hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, 1, PF, NT, WG, true, true>), g, b, 0, s, A);
+        }
+      } else if (ch == 2) {
+        hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 1, PF, NT, WG, false, true>), g, b, 0, s, A);
+      } else {
+        hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, 1, PF, NT, WG, false, true>), g, b, 0, s, A);
+      }
+      return;
+    }
+  }
   if constexpr (P == 64 && WG == 512) {
     if (A.partner) {  // round 2 of the two-round limiter (two-row tables: gm == 1)
       if (ch == 2) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 1, PF, NT, WG, true>), g, b, 0, s, A);
@@ -1253,6 +1522,19 @@ void launch_r2_plan(const MainArgs& A, const uint32_t* chunk_final, uint32_t* pi
                     hipStream_t s) {
   if (A.n_runs <= 0) return;
   hipLaunchKernelGGL(k_r2_plan, dim3(A.n_runs), dim3(64), 0, s, A, chunk_final, pieces);
+}
+
+void launch_gate_carry(const MainArgs& A, int P, int SH, int ch, int32_t* gcarry, float* gwin,
+                       hipStream_t s) {
+  if (A.n_runs <= 0 || P != 64) return;
+  const dim3 g(A.n_runs), b(64);
+  if (SH == 8) {
+    if (ch == 2) hipLaunchKernelGGL((k_gate_carry<2, 8>), g, b, 0, s, A, gcarry, gwin);
+    else hipLaunchKernelGGL((k_gate_carry<1, 8>), g, b, 0, s, A, gcarry, gwin);
+  } else if (SH == 4) {
+    if (ch == 2) hipLaunchKernelGGL((k_gate_carry<2, 4>), g, b, 0, s, A, gcarry, gwin);
+    else hipLaunchKernelGGL((k_gate_carry<1, 4>), g, b, 0, s, A, gcarry, gwin);
+  }
 }
 
 void launch_lds_gather(const LdsArgs& A, hipStream_t s) {

@@ -26,7 +26,7 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 from . import dsp
-from ._lib import (ERR_LIMITER_WAIT, ERR_PAIR_BARRIER, F32, F64, NORM_EPS, NORM_MAX,
+from ._lib import (E_UNSUPPORTED, ERR_GATE_CARRY, ERR_LIMITER_WAIT, ERR_PAIR_BARRIER, F32, F64, NORM_EPS, NORM_MAX,
                    OPT_FUSE_LIMITER, OPT_LIMITER_ROUNDS, OPT_LIMITER_SPIN, OPT_MINHOLD_SERIAL, TomatisPlanDesc, TomatisStream, check, lib,
                    ptr, stream_handle)
 
@@ -169,7 +169,7 @@ class DeviceCheckError(RuntimeError):
     """A device-side consistency check fired and the output cannot be trusted."""
 
 
-def finish_plan(plan: Plan, redo, what: str) -> int:
+def finish_plan(plan: Plan, redo, what: str, redo_gate=None) -> int:
     """Read (and clear) ``plan``'s device error word after a pass; every product
     path calls this before it returns (synchronises the current stream).
 
@@ -178,9 +178,19 @@ def finish_plan(plan: Plan, redo, what: str) -> int:
       transform with the limiter as a separate launch (the kernel's outputs and
       peaks are deterministic, so the result equals an undisturbed fused run);
       a warning says so.
+    * TOMATIS_ERR_GATE_CARRY: a run of the in-kernel gate (tomatis_stft_ola_gated)
+      found no state-fixing frame within its look-back, so the pass is invalid.
+      ``redo_gate()`` re-runs the whole pass on the two-pass chain (levels,
+      gate, transform), whose own bits are then checked as above.
     * TOMATIS_ERR_PAIR_BARRIER (or any bit after the redo): raise.
     Returns the bits first seen (0 normally)."""
     bits = plan.error_bits(reset=True)
+    if bits & ERR_GATE_CARRY:
+        if redo_gate is None:
+            raise DeviceCheckError(f"{what}: in-kernel gate carry unresolved (bits {bits:#x})")
+        redo_gate()
+        finish_plan(plan, redo, what)
+        return bits
     if bits & ERR_PAIR_BARRIER:
         raise DeviceCheckError(f"{what}: two-wave FFT exchange barrier timed out "
                                f"(device error bits {bits:#x}); the output is invalid")
@@ -382,10 +392,13 @@ class GatePipeline:
                  dynamic_range=80.0, gate_scale=1.0, gate_offset=-100, hysteresis_db=3.0,
                  fc=1000.0, slope=12.0, c1_low=15.0, c1_high=-15.0, c2_low=-15.0,
                  c2_high=15.0, up_delay_ms=250.0, n_fft=4096, hop=2048,
-                 output_gain_db=0.0, xfade_ms=None, geometry=None):
+                 output_gain_db=0.0, xfade_ms=None, geometry=None, fused_levels=True):
         """``geometry``: optional per-stream dicts (first_start, n_frames,
         out_begin, out_len, chunk_first, chunk_len, n_chunks) replacing the
-        reference schedule -- a time shard of a longer stream (timeshard.py)."""
+        reference schedule -- a time shard of a longer stream (timeshard.py).
+        ``fused_levels``: standard mode computes levels and gate states inside
+        the transform kernel (tomatis_stft_ola_gated) where the library takes
+        the shape; False, or a shape it declines, runs the two-pass chain."""
         torch = _torch()
         _check_fft(n_fft, hop, ss.ch)
         self.ss, self.n_fft, self.hop = ss, n_fft, hop
@@ -461,6 +474,9 @@ class GatePipeline:
         self.n_rows = len(rows)
         self.out_offs = out_offs
         self.g1_db, self.g2_db = g1_db, g2_db
+        self.fused_levels = bool(fused_levels) and not self.xfade
+        self.gated_used = False   # the last run() took tomatis_stft_ola_gated
+        self.gate_fallbacks = 0   # gated passes re-run on the two-pass chain
 
     def run(self, marks=None, check_device: bool = True):
         """Launch the whole chain on the current stream.
@@ -470,6 +486,36 @@ class GatePipeline:
         ``check_device``: read the plan's device error word before returning
         (one host synchronisation; ``finish_plan``).  Only a caller that checks
         once after many passes (bench.py's timed loop) turns it off."""
+        if self.fused_levels:
+            if marks:
+                marks[0].record()
+            self.gated_used = self._gated()
+            if self.gated_used:
+                if marks:
+                    marks[1].record()
+                if check_device:
+                    self.finish()
+                return self.result()
+            self.fused_levels = False  # declined: this plan's shape runs two passes
+        self._two_pass(marks)
+        if check_device:
+            self.finish()
+        return self.result()
+
+    def _gated(self) -> bool:
+        """levels + gate + transform + limiter in one pass over the input; False
+        when the library declines this plan's shape (nothing launched)."""
+        L = lib()
+        self.peaks.zero_()
+        rc = L.tomatis_stft_ola_gated(self.plan.h, ptr(self.ss.x), ptr(self.gains), self.n_rows,
+                                      ptr(self.y), ptr(self.peaks), PEAK_LIMIT, ptr(self.r),
+                                      ptr(self.states), stream_handle())
+        if rc == E_UNSUPPORTED:
+            return False
+        check(rc, "stft_ola_gated")
+        return True
+
+    def _two_pass(self, marks=None):
         L, P, hs = lib(), self.plan.h, stream_handle()
         check(L.tomatis_levels(P, ptr(self.ss.x), ptr(self.r), F32, hs), "levels")
         check(L.tomatis_gate_std(P, ptr(self.r), ptr(self.states), ptr(self.rows),
@@ -479,9 +525,6 @@ class GatePipeline:
         self._transform()
         if marks:
             marks[1].record()
-        if check_device:
-            self.finish()
-        return self.result()
 
     def _transform(self):
         """transform + OLA + per-chunk limiter (fused in-kernel when chunks are short)"""
@@ -492,6 +535,16 @@ class GatePipeline:
               "stft_ola_limited")
 
     def finish(self) -> int:
+        """Device checks of the last run() (finish_plan); an unresolved in-kernel
+        gate carry re-runs the pass on the two-pass chain (same results)."""
+        if self.gated_used:
+            def redo_gate():
+                self.gated_used = False
+                self.gate_fallbacks += 1
+                self._two_pass()
+            # a limiter-wait redo of the gated pass: the transform alone cannot
+            # recompute states, so the two-pass chain runs with the unfused limiter
+            return finish_plan(self.plan, redo_gate, "GatePipeline", redo_gate=redo_gate)
         return finish_plan(self.plan, self._transform, "GatePipeline")
 
     def result(self) -> Result:
