@@ -87,14 +87,16 @@ def test_validator_spectrum_criterion_fullsize():
     n = SR * SECS
     ss = E.StreamSet.synthetic(1, n, 2, SR, seed0=1000)
     # re-envelope the synthetic noise: loud half (-20 dBFS) -> -30, quiet half
-    # (-60 dBFS) -> -50 (phase of synth.envelope: quiet first, 1.5 s each)
+    # (-60 dBFS) -> -50 (phase of synth.envelope: quiet first, 1.5 s each; the
+    # quiet half opens with the 10 ms loud -> quiet ramp, which stays at -10 dB)
     idx = torch.arange(n, device=ss.x.device)
     half = (3 * SR) // 2
-    g = torch.where(torch.remainder(idx, 3 * SR) < half,
+    ph = torch.remainder(idx, 3 * SR)
+    g = torch.where((ph >= SR // 100) & (ph < half),
                     torch.tensor(10.0 ** (10 / 20), device=ss.x.device),
                     torch.tensor(10.0 ** (-10 / 20), device=ss.x.device)).to(torch.float32)
     x2 = ss.x[:n * 2].view(n, 2) * g[:, None]
-    del idx, g
+    del idx, ph, g
     ss2 = E.StreamSet(x=x2.reshape(-1).contiguous(), offs=[0], lens=[n], ch=2, sr=SR)
     pipe = E.GatePipeline(ss2, gate_ui=50, n_fft=NFFT, hop=HOP)
     res = pipe.run()

@@ -102,14 +102,22 @@ __device__ __forceinline__ void xsync(cf* buf = nullptr, uint32_t* err = nullptr
   }
 }
 
-// exchange-2 column of element (a, c) in a row: XOR swizzle a ^ g(c) with
-// g(c) = (c & 7) ^ ((c >> 2) & 2).  For P = 64 (c < 8) g(c) = c; for P = 128
-// (c < 16) plain c & 7 maps c and c + 8 onto the same banks (2-way conflicts
-// on the exchange-2 reads, 16.5 % of LDS cycles measured on C5x); folding c's
-// bit 3 into bit 1 makes exchanges 2 and 3 conflict-free for both (checked
-// against the gfx950 lane-group / bank rules of every exchange instruction,
-// MI355X_MICROARCH.md "LDS")
-__device__ __forceinline__ int x2col(int a, int c) { return 8 * c + (a ^ ((c & 7) ^ ((c >> 2) & 2))); }
+// exchange-2 column of element (a, c) in a row: XOR swizzle a ^ g(c).
+// P = 64 (c < 8): g(c) = c.  P = 128 (c < 16): the exchange-2 reads and
+// exchange-3 writes of one element index go out as ds_read2st64_b64 /
+// ds_write2st64_b64 (the two rounds' rows in one instruction), whose 16-lane
+// groups (c = 0..15 at one row) bank by dword mod 32, i.e. by
+// (c & 1, a ^ g(c)): g must be a bijection on the even and on the odd c.
+// g(c) = (c >> 1) ^ 4 (c & 1) is (plain c & 7 maps c and c + 8 onto the same
+// banks: 2-way conflicts, 16.5 % of the LDS cycles of C5x).  The other
+// exchange instructions bank on (q, a) and are conflict-free for any g
+// (tools/lds_banks.py checks every exchange against the gfx950 lane-group /
+// bank rules, MI355X_MICROARCH.md "LDS").
+template <int P>
+__device__ __forceinline__ int x2col(int a, int c) {
+  if constexpr (P > 64) return 8 * c + (a ^ (((c >> 1) & 7) ^ ((c & 1) << 2)));
+  return 8 * c + (a ^ (c & 7));
+}
 
 // forward FFT.  v: 32 registers (input x[L + P*n2]); out: bin layout above.
 // twN: LDS W_N^{n1*k2} in lane-pair layout [k2/2][n1][k2&1] (16-B aligned);
@@ -181,7 +189,7 @@ __device__ __forceinline__ void fft_fwd(cf (&v)[NR], int L, const cf* twN, const
     constexpr int R = decltype(rr)::value;
     sfor<0, PB>([&](auto cc) {
       constexpr int C = decltype(cc)::value;
-      buf[q1 * RW + x2col(a1, C)] = v[R * PB + C];
+      buf[q1 * RW + x2col<P>(a1, C)] = v[R * PB + C];
     });
     xsync<P, NR>(buf, err);
     sfor<0, PB / 8>([&](auto jj) {
@@ -189,7 +197,7 @@ __device__ __forceinline__ void fft_fwd(cf (&v)[NR], int L, const cf* twN, const
       const int row = q3 + 8 * JJ;
       sfor<0, 8>([&](auto aa) {
         constexpr int A = decltype(aa)::value;
-        v[R * PB + JJ * 8 + A] = buf[row * RW + x2col(A, c3)];
+        v[R * PB + JJ * 8 + A] = buf[row * RW + x2col<P>(A, c3)];
       });
     });
     xsync<P, NR>(buf, err);
@@ -247,13 +255,13 @@ __device__ __forceinline__ void fft_inv(cf (&v)[NR], int L, const cf* twN, const
       const int row = q3 + 8 * JJ;
       sfor<0, 8>([&](auto aa) {
         constexpr int A = decltype(aa)::value;
-        buf[row * RW + x2col(A, c3)] = v[R * PB + JJ * 8 + A];
+        buf[row * RW + x2col<P>(A, c3)] = v[R * PB + JJ * 8 + A];
       });
     });
     xsync<P, NR>(buf, err);
     sfor<0, PB>([&](auto cc) {
       constexpr int C = decltype(cc)::value;
-      v[R * PB + C] = buf[q1 * RW + x2col(a1, C)];
+      v[R * PB + C] = buf[q1 * RW + x2col<P>(a1, C)];
     });
     xsync<P, NR>(buf, err);
   });
