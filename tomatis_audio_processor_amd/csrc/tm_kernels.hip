@@ -610,7 +610,11 @@ __device__ __forceinline__ uint16_t xfade_row(double a, int xf) {
   return (a < 0.5) ? 0 : 1;
 }
 
-// pass 1: one thread per segment: sync frame, alpha from it to the segment end
+// pass 1: one wave per segment: sync frame, alpha from it to the segment end.
+// The segment's states are staged in LDS by all lanes; the recurrence runs in
+// lane 0 from LDS (four frames per read); alpha and rows go back out through
+// LDS as coalesced stores (one thread per segment walking global memory frame
+// by frame took 0.35 ms on C5x: 440 segments = 7 waves on the chip)
 __global__ __launch_bounds__(64) void k_alpha_sync(const TomatisStream* __restrict__ st,
                                                    const GateSeg* __restrict__ segs, int nseg,
                                                    const uint8_t* __restrict__ states, int xf,
@@ -618,44 +622,88 @@ __global__ __launch_bounds__(64) void k_alpha_sync(const TomatisStream* __restri
                                                    double* __restrict__ alpha,
                                                    int32_t* __restrict__ seg_q,
                                                    double* __restrict__ seg_final) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ __attribute__((aligned(16))) uint8_t s_st[kSeg];
+  __shared__ double s_a[kSeg];
+  __shared__ int s_q;
+  const int i = blockIdx.x;
   if (i >= nseg) return;
+  const int L = threadIdx.x;
   const GateSeg G = segs[i];
   const TomatisStream S = st[G.s];
   const uint8_t* stt = states + S.frame_base;
   const int J = xf + 2;
   const double step = xf > 0 ? 1.0 / xf : 1.0;
-  // run of equal states ending just before k0 (frames < 0 are C1 forever)
+  for (int j = L; j < G.nf; j += 64) s_st[j] = stt[G.k0 + j];
+  // run of equal states ending just before k0 (frames < 0 are C1 forever):
+  // lanes test 64 earlier frames at a time
   uint8_t prev = 1;
   int run = J;
   if (G.k0 > 0) {
     prev = stt[G.k0 - 1];
     run = 1;
-    int64_t k = G.k0 - 2;
-    for (; k >= 0 && run < J && stt[k] == prev; --k) ++run;
-    if (k < 0 && run < J && prev == 1) run = J;  // reaches the C1 pre-history
+    bool open = true;  // the run has not met a different state yet
+    for (int64_t base = G.k0 - 2; open && run < J && base >= 0; base -= 64) {
+      const int64_t k = base - L;
+      const bool diff = (k >= 0) && stt[k] != prev;
+      const uint64_t m = __ballot(diff);
+      const int avail = (int)min<int64_t>(64, base + 1);  // frames base .. base - avail + 1
+      const int same = m ? __builtin_ctzll(m) : avail;
+      run = min(run + same, J);
+      if (m || same < 64) open = false;
+      if (!m && base - 64 < 0 && same == avail && run < J && prev == 1) run = J;  // C1 pre-history
+    }
+    if (open && run < J && prev == 1 && G.k0 - 1 - (run - 1) <= 0) run = J;
   }
-  int q = G.nf;
-  for (int j = 0; j < G.nf; ++j) {
-    const uint8_t t = stt[G.k0 + j];
-    run = (t == prev) ? min(run + 1, J) : 1;
-    prev = t;
-    if (xf == 0 || run >= J) {
-      q = j;
-      break;
+  __syncthreads();
+  if (L == 0) {
+    // 16 states per LDS read (the loops are latency chains in one lane)
+    const uint4* s4 = reinterpret_cast<const uint4*>(s_st);
+    auto st_of = [](const uint4& w, int u) -> uint8_t {
+      const uint32_t d = u < 4 ? w.x : (u < 8 ? w.y : (u < 12 ? w.z : w.w));
+      return (uint8_t)(d >> (8 * (u & 3)));
+    };
+    int q = G.nf;
+    for (int b = 0; b * 16 < G.nf && q == G.nf; ++b) {
+      const uint4 w = s4[b];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int j = b * 16 + u;
+        if (j < G.nf && q == G.nf) {
+          const uint8_t t = st_of(w, u);
+          run = (t == prev) ? min(run + 1, J) : 1;
+          prev = t;
+          if (xf == 0 || run >= J) q = j;
+        }
+      }
+    }
+    s_q = q;
+    seg_q[i] = q;
+    if (q < G.nf) {
+      double a = s_st[q] == 1 ? 0.0 : 1.0;
+      s_a[q] = a;
+      for (int b = (q + 1) >> 4; b * 16 < G.nf; ++b) {
+        const uint4 w = s4[b];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int j = b * 16 + u;
+          if (j > q && j < G.nf) {
+            const double tgt = st_of(w, u) == 1 ? 0.0 : 1.0;
+            a = (xf > 0) ? alpha_step(a, tgt, step) : tgt;
+            s_a[j] = a;
+          }
+        }
+      }
+      seg_final[i] = a;
     }
   }
-  seg_q[i] = q;
-  if (q == G.nf) return;
-  double a = stt[G.k0 + q] == 1 ? 0.0 : 1.0;
-  for (int j = q; j < G.nf; ++j) {
+  __syncthreads();
+  const int q = s_q;
+  for (int j = q + L; j < G.nf; j += 64) {
     const int64_t f = S.frame_base + G.k0 + j;
-    const double tgt = stt[G.k0 + j] == 1 ? 0.0 : 1.0;
-    if (j > q) a = (xf > 0) ? alpha_step(a, tgt, step) : tgt;
+    const double a = s_a[j];
     if (alpha) alpha[f] = a;
     rows[f] = xfade_row(a, xf);
   }
-  seg_final[i] = a;
 }
 
 // pass 2: one thread per stream: carry-in alpha of every segment
@@ -684,7 +732,8 @@ __global__ void k_alpha_chain(const TomatisStream* __restrict__ st, int n_stream
   }
 }
 
-// pass 3: one thread per segment: the frames before its sync frame
+// pass 3: one wave per segment: the frames before its sync frame (all of them
+// when the segment has none), from the carry-in; staged through LDS as pass 1
 __global__ __launch_bounds__(64) void k_alpha_prefix(const TomatisStream* __restrict__ st,
                                                      const GateSeg* __restrict__ segs, int nseg,
                                                      const uint8_t* __restrict__ states, int xf,
@@ -692,16 +741,39 @@ __global__ __launch_bounds__(64) void k_alpha_prefix(const TomatisStream* __rest
                                                      const double* __restrict__ carry_in,
                                                      uint16_t* __restrict__ rows,
                                                      double* __restrict__ alpha) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ __attribute__((aligned(16))) uint8_t s_st[kSeg];
+  __shared__ double s_a[kSeg];
+  const int i = blockIdx.x;
   if (i >= nseg) return;
+  const int q = seg_q[i];
+  if (q == 0) return;
+  const int L = threadIdx.x;
   const GateSeg G = segs[i];
   const TomatisStream S = st[G.s];
   const double step = xf > 0 ? 1.0 / xf : 1.0;
-  double a = carry_in[i];
-  for (int j = 0; j < seg_q[i]; ++j) {
+  for (int j = L; j < q; j += 64) s_st[j] = states[S.frame_base + G.k0 + j];
+  __syncthreads();
+  if (L == 0) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(s_st);
+    double a = carry_in[i];
+    for (int b = 0; b * 16 < q; ++b) {
+      const uint4 w = s4[b];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int j = b * 16 + u;
+        if (j < q) {
+          const uint32_t d = u < 4 ? w.x : (u < 8 ? w.y : (u < 12 ? w.z : w.w));
+          const double tgt = (uint8_t)(d >> (8 * (u & 3))) == 1 ? 0.0 : 1.0;
+          a = (xf > 0) ? alpha_step(a, tgt, step) : tgt;
+          s_a[j] = a;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int j = L; j < q; j += 64) {
     const int64_t f = S.frame_base + G.k0 + j;
-    const double tgt = states[f] == 1 ? 0.0 : 1.0;
-    a = (xf > 0) ? alpha_step(a, tgt, step) : tgt;
+    const double a = s_a[j];
     if (alpha) alpha[f] = a;
     rows[f] = xfade_row(a, xf);
   }
@@ -2373,7 +2445,7 @@ int tomatis_gate_std(tomatis_plan_t p, const float* r, uint8_t* states, uint16_t
           hipMalloc(reinterpret_cast<void**>(&p->acin), (size_t)p->n_segs * sizeof(double)))
         return TOMATIS_E_NOMEM;
     }
-    const unsigned gs = (unsigned)((p->n_segs + 63) / 64);
+    const unsigned gs = (unsigned)p->n_segs;  // one wave per segment
     hipLaunchKernelGGL(k_alpha_sync, dim3(gs), dim3(64), 0, s, p->st, p->segs, p->n_segs, states,
                        nxf, rows, alpha_out, p->aq, p->afin);
     hipLaunchKernelGGL(k_alpha_chain, dim3((p->n_streams + 63) / 64), dim3(64), 0, s, p->st,
