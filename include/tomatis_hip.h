@@ -15,6 +15,8 @@
  *   src/process_tomatis_adaptive.py:57-84        tomatis_levels
  *       (compute_frame_levels)
  *   src/process_tomatis.py:373-385 (gate)        tomatis_gate_std
+ *   src/process_tomatis.py:369-406 (levels,      tomatis_stft_ola_gated
+ *       gate and transform in one pass)           (+ tomatis_gate_lookback)
  *   src/process_tomatis_xfade.py:237-274         tomatis_gate_std (+alpha rows)
  *   src/process_tomatis_adaptive.py:87-154       tomatis_minhold_bisect
  *       (simulate_gate, find_optimal_threshold)
@@ -60,7 +62,7 @@
 extern "C" {
 #endif
 
-#define TOMATIS_ABI_VERSION 5
+#define TOMATIS_ABI_VERSION 6
 
 #define TOMATIS_OK 0
 #define TOMATIS_E_ARG (-1)        /* bad argument */
@@ -257,6 +259,15 @@ int tomatis_stft_ola_limited_edges(tomatis_plan_t plan, const float* x, const fl
 int tomatis_stft_ola_gated(tomatis_plan_t plan, const float* x, const float* gain_rows,
                            int32_t n_rows, float* y, uint32_t* chunk_peak_bits, float limit,
                            float* r_out, uint8_t* states_out, void* hip_stream);
+/* The two launches of tomatis_stft_ola_gated separately (the caller times the
+ * transform alone): tomatis_gate_lookback runs the look-back pre-kernel on x;
+ * tomatis_stft_ola_gated_after_lookback then runs the transform on the same x,
+ * on the same stream, with no other gated call of this plan in between. */
+int tomatis_gate_lookback(tomatis_plan_t plan, const float* x, void* hip_stream);
+int tomatis_stft_ola_gated_after_lookback(tomatis_plan_t plan, const float* x,
+                                          const float* gain_rows, int32_t n_rows, float* y,
+                                          uint32_t* chunk_peak_bits, float limit, float* r_out,
+                                          uint8_t* states_out, void* hip_stream);
 /* The limiter on the edge chunks of edge_mask only. */
 int tomatis_apply_limiter_edges(tomatis_plan_t plan, float* y, const uint32_t* chunk_peak_bits,
                                 float limit, int32_t edge_mask, void* hip_stream);

@@ -14,7 +14,7 @@ import ctypes as C
 import os
 
 LIB_NAME = "libtomatis_hip.so"
-ABI_VERSION = 5  # include/tomatis_hip.h TOMATIS_ABI_VERSION
+ABI_VERSION = 6  # include/tomatis_hip.h TOMATIS_ABI_VERSION
 GATE_SEGMENT = 1024      # TOMATIS_GATE_SEGMENT
 GATE_NONE = -536870912   # TOMATIS_GATE_NONE
 ERR_LIMITER_WAIT = 1     # TOMATIS_ERR_LIMITER_WAIT
@@ -100,6 +100,9 @@ _SIGS = {
                                                  C.c_int32, _P]),
     "tomatis_apply_limiter_edges": (C.c_int, [_P, _P, _P, C.c_float, C.c_int32, _P]),
     "tomatis_stft_ola_gated": (C.c_int, [_P, _P, _P, C.c_int32, _P, _P, C.c_float, _P, _P, _P]),
+    "tomatis_gate_lookback": (C.c_int, [_P, _P, _P]),
+    "tomatis_stft_ola_gated_after_lookback": (C.c_int, [_P, _P, _P, C.c_int32, _P, _P, C.c_float,
+                                                        _P, _P, _P]),
     "tomatis_ts_summary": (C.c_int, [_P, _P, C.c_int32, C.c_int32, _P, _P]),
     "tomatis_ts_gate": (C.c_int, [_P, _P, _P, C.c_int32, C.c_int32, _P, _P, _P]),
     "tomatis_plan_error": (C.c_int, [_P, _P]),

@@ -2573,7 +2573,35 @@ int tomatis_minhold_bisect(tomatis_plan_t p, const double* levels, const double*
 struct GateOut {
   float* r;
   uint8_t* states;
+  bool lookback_done;  // tomatis_gate_lookback ran for this input on this stream
 };
+
+// per-run carry-in state id and leaf window of the fused gate (k_gate_carry)
+static int gate_lookback(tomatis_plan_s* p, const float* x, hipStream_t s) {
+  if (p->n_runs > p->gate_cap) {
+    dfree(p->gate_carry);
+    dfree(p->gate_win);
+    p->gate_carry = nullptr;
+    p->gate_win = nullptr;
+    p->gate_cap = 0;
+    if (hipMalloc(reinterpret_cast<void**>(&p->gate_carry), (size_t)p->n_runs * sizeof(int32_t)) ||
+        hipMalloc(reinterpret_cast<void**>(&p->gate_win), (size_t)p->n_runs * 16 * sizeof(float)))
+      return TOMATIS_E_NOMEM;
+    p->gate_cap = p->n_runs;
+  }
+  if (p->n_runs == 0) return TOMATIS_OK;
+  MainArgs A{};
+  A.x = x;
+  A.st = p->st;
+  A.runs = p->runs;
+  A.n_runs = p->n_runs;
+  A.rmax = p->rmax;
+  A.hop = p->d.hop;
+  A.ch = p->d.ch;
+  A.gate_D = p->d.up_delay_frames;
+  launch_gate_carry(A, p->P, p->SH, p->d.ch, p->gate_carry, p->gate_win, s);
+  return launch_check();
+}
 
 static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, int32_t n_rows,
                          const uint16_t* rows, float* y, uint32_t* peaks, float limit,
@@ -2684,25 +2712,15 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
   if (gate) {
     // per run: the carry-in state id and leaf window (k_gate_carry), then the
     // transform computes every frame's r and state from the input it loads
-    if (p->n_runs > p->gate_cap) {
-      dfree(p->gate_carry);
-      dfree(p->gate_win);
-      p->gate_carry = nullptr;
-      p->gate_win = nullptr;
-      p->gate_cap = 0;
-      if (hipMalloc(reinterpret_cast<void**>(&p->gate_carry), (size_t)p->n_runs * sizeof(int32_t)) ||
-          hipMalloc(reinterpret_cast<void**>(&p->gate_win), (size_t)p->n_runs * 16 * sizeof(float)))
-        return TOMATIS_E_NOMEM;
-      p->gate_cap = p->n_runs;
+    if (!gate->lookback_done || p->n_runs > p->gate_cap) {
+      const int rc = gate_lookback(p, x, s);
+      if (rc) return rc;
     }
     A.gated = 1;
     A.r_out = gate->r;
     A.st_out = gate->states;
     A.gcarry = p->gate_carry;
     A.gwin = p->gate_win;
-    launch_gate_carry(A, p->P, p->SH, p->d.ch, p->gate_carry, p->gate_win, s);
-    const int rc = launch_check();
-    if (rc) return rc;
   }
   if (limit > 0.f) {
     if (!p->chunk_done) return TOMATIS_E_UNSUPPORTED;
@@ -2824,13 +2842,19 @@ static bool gated_eligible(const tomatis_plan_s* p) {
   return true;
 }
 
-int tomatis_stft_ola_gated(tomatis_plan_t p, const float* x, const float* gains, int32_t n_rows,
-                           float* y, uint32_t* peaks, float limit, float* r_out,
-                           uint8_t* states_out, void* hs) {
+int tomatis_gate_lookback(tomatis_plan_t p, const float* x, void* hs) {
+  if (!p || !x) return TOMATIS_E_ARG;
+  if (!gated_eligible(p)) return TOMATIS_E_UNSUPPORTED;
+  return gate_lookback(p, x, (hipStream_t)hs);
+}
+
+static int stft_ola_gated(tomatis_plan_t p, const float* x, const float* gains, int32_t n_rows,
+                          float* y, uint32_t* peaks, float limit, float* r_out,
+                          uint8_t* states_out, bool lookback_done, void* hs) {
   if (!p || !x || !gains || !y || !peaks || !r_out || !states_out || n_rows != 2 || limit < 0.f)
     return TOMATIS_E_ARG;
   if (!gated_eligible(p)) return TOMATIS_E_UNSUPPORTED;
-  const GateOut g{r_out, states_out};
+  const GateOut g{r_out, states_out, lookback_done};
   if (!(limit > 0.f)) return stft_ola_impl(p, x, gains, n_rows, nullptr, y, peaks, 0.f, hs, &g);
   const bool fuse = p->chunk_done && p->fuse_span > 0 && p->fuse_enabled &&
                     p->fuse_span <= fuse_max_span(p) && dev_opt(TOMATIS_DEV_FUSE_LIMITER, 1) != 0;
@@ -2838,6 +2862,18 @@ int tomatis_stft_ola_gated(tomatis_plan_t p, const float* x, const float* gains,
   int rc = stft_ola_impl(p, x, gains, n_rows, nullptr, y, peaks, 0.f, hs, &g);
   if (!rc) rc = limiter_launch(p, y, peaks, limit, 0, 0, hs);
   return rc;
+}
+
+int tomatis_stft_ola_gated(tomatis_plan_t p, const float* x, const float* gains, int32_t n_rows,
+                           float* y, uint32_t* peaks, float limit, float* r_out,
+                           uint8_t* states_out, void* hs) {
+  return stft_ola_gated(p, x, gains, n_rows, y, peaks, limit, r_out, states_out, false, hs);
+}
+
+int tomatis_stft_ola_gated_after_lookback(tomatis_plan_t p, const float* x, const float* gains,
+                                          int32_t n_rows, float* y, uint32_t* peaks, float limit,
+                                          float* r_out, uint8_t* states_out, void* hs) {
+  return stft_ola_gated(p, x, gains, n_rows, y, peaks, limit, r_out, states_out, true, hs);
 }
 
 int tomatis_stft_ola_limited(tomatis_plan_t p, const float* x, const float* gains,

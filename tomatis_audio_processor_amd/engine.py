@@ -487,9 +487,7 @@ class GatePipeline:
         (one host synchronisation; ``finish_plan``).  Only a caller that checks
         once after many passes (bench.py's timed loop) turns it off."""
         if self.fused_levels:
-            if marks:
-                marks[0].record()
-            self.gated_used = self._gated()
+            self.gated_used = self._gated(marks)
             if self.gated_used:
                 if marks:
                     marks[1].record()
@@ -502,17 +500,22 @@ class GatePipeline:
             self.finish()
         return self.result()
 
-    def _gated(self) -> bool:
-        """levels + gate + transform + limiter in one pass over the input; False
-        when the library declines this plan's shape (nothing launched)."""
-        L = lib()
-        self.peaks.zero_()
-        rc = L.tomatis_stft_ola_gated(self.plan.h, ptr(self.ss.x), ptr(self.gains), self.n_rows,
-                                      ptr(self.y), ptr(self.peaks), PEAK_LIMIT, ptr(self.r),
-                                      ptr(self.states), stream_handle())
+    def _gated(self, marks=None) -> bool:
+        """levels + gate + transform + limiter in one pass over the input (the
+        look-back pre-kernel, then the transform); False when the library
+        declines this plan's shape (nothing launched).  ``marks`` bracket the
+        transform launch."""
+        L, hs = lib(), stream_handle()
+        rc = L.tomatis_gate_lookback(self.plan.h, ptr(self.ss.x), hs)
         if rc == E_UNSUPPORTED:
             return False
-        check(rc, "stft_ola_gated")
+        check(rc, "gate_lookback")
+        self.peaks.zero_()
+        if marks:
+            marks[0].record()
+        check(L.tomatis_stft_ola_gated_after_lookback(
+            self.plan.h, ptr(self.ss.x), ptr(self.gains), self.n_rows, ptr(self.y),
+            ptr(self.peaks), PEAK_LIMIT, ptr(self.r), ptr(self.states), hs), "stft_ola_gated")
         return True
 
     def _two_pass(self, marks=None):
