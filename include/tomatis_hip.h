@@ -346,6 +346,28 @@ int32_t tomatis_plan_limiter_rounds(tomatis_plan_t plan);
 #define TOMATIS_DEV_FUSED_LEVELS 14    /* 0: tomatis_stft_ola_gated declines (host two-pass) */
 int tomatis_set_dev_option(int32_t key, int32_t value);
 
+/* FLAC frames encoded on the device (row f1 egress; src/process_tomatis.py:
+ * 242-251,357 write the output through libsndfile's FLAC PCM_24 encoder).
+ * Byte for byte the frames tomatis_flac_encode (include/tomatis_flac.h) writes
+ * for the same interleaved int32 PCM: 4096-sample blocks, frame number = block
+ * index.  1-2 channels, 4-24 bits (TOMATIS_E_UNSUPPORTED otherwise).
+ *   tomatis_flacd_workspace_bytes: device workspace for `frames` (plans).
+ *   tomatis_flacd_plan: per block its plan (into ws) and frame size in bytes
+ *     into frame_bytes[block] (device, uint32); 0xFFFFFFFF marks a block with a
+ *     sample outside the bit depth, 0xFFFFFFFE one the device writer cannot
+ *     hold (encode the stream on the host then).
+ *   tomatis_flacd_write: every frame at byte frame_off[block] (device, int64,
+ *     the exclusive prefix sum of the sizes) of `out`, which the caller zeroes
+ *     and sizes to the total rounded up to a multiple of 4 bytes.
+ * The caller writes "fLaC" + STREAMINFO (block / frame size extremes, total
+ * samples, MD5 zero) in front, as tomatis_flac_encode does. */
+int64_t tomatis_flacd_workspace_bytes(int64_t frames, int32_t ch);
+int tomatis_flacd_plan(const int32_t* pcm, int64_t frames, int32_t ch, int32_t bps, void* ws,
+                       uint32_t* frame_bytes, void* hip_stream);
+int tomatis_flacd_write(const int32_t* pcm, int64_t frames, int32_t ch, int32_t bps,
+                        const void* ws, const int64_t* frame_off, uint8_t* out,
+                        void* hip_stream);
+
 /* max |x| over n floats as float bits (out zeroed by caller). */
 int tomatis_absmax(const float* x, int64_t n, uint32_t* out_bits, void* hip_stream);
 

@@ -101,6 +101,9 @@ _SIGS = {
     "tomatis_apply_limiter_edges": (C.c_int, [_P, _P, _P, C.c_float, C.c_int32, _P]),
     "tomatis_stft_ola_gated": (C.c_int, [_P, _P, _P, C.c_int32, _P, _P, C.c_float, _P, _P, _P]),
     "tomatis_gate_lookback": (C.c_int, [_P, _P, _P]),
+    "tomatis_flacd_workspace_bytes": (C.c_int64, [C.c_int64, C.c_int32]),
+    "tomatis_flacd_plan": (C.c_int, [_P, C.c_int64, C.c_int32, C.c_int32, _P, _P, _P]),
+    "tomatis_flacd_write": (C.c_int, [_P, C.c_int64, C.c_int32, C.c_int32, _P, _P, _P, _P]),
     "tomatis_stft_ola_gated_after_lookback": (C.c_int, [_P, _P, _P, C.c_int32, _P, _P, C.c_float,
                                                         _P, _P, _P]),
     "tomatis_ts_summary": (C.c_int, [_P, _P, C.c_int32, C.c_int32, _P, _P]),

@@ -1,13 +1,14 @@
 """Build ``libtomatis_hip.so`` in-tree with hipcc for gfx950 (no cmake/ninja needed).
 
-Three translation units, compiled in parallel and linked into one C-ABI library:
+Four translation units, compiled in parallel and linked into one C-ABI library:
 
 * ``tm_kernels.hip``   levels, gate, limiter, plan and the ``extern "C"`` entry points;
 * ``tm_transform.hip`` the fused transform kernels (FMA contraction on;
   ``TOMATIS_TRANSFORM_SCHED`` selects another LLVM machine scheduler for
   experiments — measured within 1 % of the default);
 * ``tm_analysis.hip``  analysis spectra for the validators / calibration tools
-  (SURVEY.md §8 rows f3/f4).
+  (SURVEY.md §8 rows f3/f4);
+* ``tm_flacenc.hip``   FLAC frames encoded on the device (row f1's egress).
 """
 from __future__ import annotations
 
@@ -28,6 +29,7 @@ UNITS = {  # source -> extra flags
     "tm_transform.hip": ["-ffp-contract=fast"] +
                         (["-mllvm", f"-amdgpu-sched-strategy={SCHED}"] if SCHED else []),
     "tm_analysis.hip": [],
+    "tm_flacenc.hip": [],
 }
 DEPS = [os.path.join(CSRC, f) for f in (*UNITS, "tm_common.h", "tm_fft.h", "tm_shared.h",
                                         "tm_lds_fft.h", "tm_host_dsp.h", "tm_gate.h")] + \

@@ -8,12 +8,15 @@ ingest   FLAC bytes -> K byte ranges decoded on host threads into one
          page-locked int32 block (``tomatis_flac_decode_bytes``); each range's
          samples are DMA'd to HBM on a copy stream while the next range
          decodes; int -> float32 (libsndfile's 2^(bps-1) rule) on the device.
-egress   float32 -> PCM_24 on the device (``tomatis_float_to_pcm``), then
-         segments of 2^22 frames D2H into two alternating page-locked
-         buffers on a copy stream, each encoded on host threads
-         (``tomatis_flac_enc_push``) while the next one is in flight, and
-         written to the file by a writer thread while later segments encode;
-         the stream is byte-identical to a whole-buffer encode.
+egress   float32 -> PCM_24 on the device (``tomatis_float_to_pcm``), FLAC
+         frames encoded on the device (``tomatis_flacd_plan`` / ``_write``:
+         per 4096-sample block plan and exact size, host prefix sum of the
+         sizes, frames written at their offsets), then the compressed bytes
+         D2H in pieces through two page-locked buffers while the file is
+         written.  Shapes the device encoder declines: segments of 2^22 frames
+         D2H, encoded on host threads (``tomatis_flac_enc_push``) while the next
+         one is in flight, written by a writer thread.  Both paths give the
+         bytes of a whole-buffer host encode.
 
 WAV files (and any format when libsndfile is importable) go through
 ``audio_io`` on the host as before; the reference's FLAC -> WAV fallback on an
@@ -229,8 +232,82 @@ def _encode_segments(y, n, ch, sr, bps, sink, timer=None):
     return bytes(hdr)
 
 
-def encode_flac_device(y, n: int, ch: int, sr: int, bps: int = 24, timer=None) -> bytes:
-    """FLAC stream of the device float32 samples y [n*ch] at ``bps`` bits."""
+FLAC_BLOCK = 4096             # tm_flac.cpp kBlock / tm_flacenc.hip kFdBlock
+D2H_CHUNK = 1 << 26          # device-encoded bytes per D2H copy while the file is written
+
+
+def _streaminfo_header(frames, ch, sr, bps, min_fs, max_fs, min_bs, max_bs) -> bytes:
+    """"fLaC" + the STREAMINFO block tm_flac.cpp writes (MD5 zero)."""
+    if frames == 0:
+        min_fs = max_fs = 0
+        min_bs = max_bs = FLAC_BLOCK
+    fields = [(FLAC_BLOCK if frames > FLAC_BLOCK else max(16, min_bs), 16),
+              (max(16, max_bs), 16), (min_fs, 24), (max_fs, 24), (sr, 20), (ch - 1, 3),
+              (bps - 1, 5), (frames >> 32, 4), (frames & 0xFFFFFFFF, 32)]
+    acc = 0
+    for v, nb in fields:
+        acc = (acc << nb) | (v & ((1 << nb) - 1))
+    return b"fLaC" + bytes([0x80, 0, 0, 34]) + acc.to_bytes(18, "big") + bytes(16)
+
+
+def _device_frames(yi, n: int, ch: int, bps: int):
+    """FLAC frames of device int32 PCM yi [n*ch] encoded on the device
+    (tomatis_flacd_*, byte-identical to the host encoder): (uint8 device
+    tensor of the frames, total bytes, (min_fs, max_fs, min_bs, max_bs)), or
+    None when the device encoder declines (shape, or a block it cannot hold)."""
+    torch = _torch()
+    L, hs = lib(), stream_handle()
+    if not (1 <= ch <= 2 and 4 <= bps <= 24) or n == 0:
+        return None
+    nblk = (n + FLAC_BLOCK - 1) // FLAC_BLOCK
+    ws = torch.empty(int(L.tomatis_flacd_workspace_bytes(n, ch)), dtype=torch.uint8,
+                     device="cuda")
+    sizes = torch.empty(nblk, dtype=torch.int32, device="cuda")
+    check(L.tomatis_flacd_plan(ptr(yi), n, ch, bps, ptr(ws), ptr(sizes), hs), "flacd_plan")
+    sz = sizes.cpu().numpy().view(np.uint32).astype(np.int64)   # synchronises
+    if (sz >= 0xFFFFFFFE).any():
+        return None
+    off = np.zeros(nblk, np.int64)
+    np.cumsum(sz[:-1], out=off[1:])
+    total = int(off[-1] + sz[-1])
+    out = torch.zeros((total + 7) // 4 * 4, dtype=torch.uint8, device="cuda")
+    off_d = torch.from_numpy(off).to("cuda")
+    check(L.tomatis_flacd_write(ptr(yi), n, ch, bps, ptr(ws), ptr(off_d), ptr(out), hs),
+          "flacd_write")
+    bs_last = n - (nblk - 1) * FLAC_BLOCK
+    stats = (int(sz.min()), int(sz.max()), min(FLAC_BLOCK, bs_last), FLAC_BLOCK if nblk > 1 else bs_last)
+    return out, total, stats
+
+
+def encode_flac_device_frames(y, n: int, ch: int, sr: int, bps: int = 24):
+    """The FLAC stream of device float32 samples y [n*ch] encoded on the device,
+    as (header bytes, uint8 device tensor of the frames, frame bytes), or None
+    when the device encoder declines (the host encoder then applies)."""
+    torch = _torch()
+    yi = torch.empty(max(1, n * ch), dtype=torch.int32, device="cuda")
+    check(lib().tomatis_float_to_pcm(ptr(y), n * ch, bps, ptr(yi), stream_handle()),
+          "float_to_pcm")
+    r = _device_frames(yi, n, ch, bps)
+    if r is None:
+        return None
+    out, total, (min_fs, max_fs, min_bs, max_bs) = r
+    return _streaminfo_header(n, ch, sr, bps, min_fs, max_fs, min_bs, max_bs), out, total
+
+
+def encode_flac_device(y, n: int, ch: int, sr: int, bps: int = 24, timer=None,
+                       device_encoder: bool = True) -> bytes:
+    """FLAC stream of the device float32 samples y [n*ch] at ``bps`` bits
+    (encoded on the device when it takes the shape, else on host threads; the
+    bytes are the same)."""
+    if device_encoder:
+        t0 = time.perf_counter()
+        r = encode_flac_device_frames(y, n, ch, sr, bps)
+        if r is not None:
+            hdr, out, total = r
+            b = hdr + out[:total].cpu().numpy().tobytes()
+            if timer is not None:
+                timer.add("encode+d2h", t0)
+            return b
     parts = []
 
     def take(b):
@@ -243,14 +320,61 @@ def encode_flac_device(y, n: int, ch: int, sr: int, bps: int = 24, timer=None) -
     return hdr + b"".join(parts)
 
 
-def write_device(out_path: str, y, n: int, ch: int, sr: int, log=print, timer=None):
+def _write_device_frames(f, y, n, ch, sr, timer=None) -> bool:
+    """Device-encoded FLAC into the open file f: header, then the frames in
+    D2H_CHUNK pieces through two page-locked buffers (the copy of piece k + 1
+    overlaps the write of piece k).  False when the device encoder declines."""
+    torch = _torch()
+    t0 = time.perf_counter()
+    r = encode_flac_device_frames(y, n, ch, sr, 24)
+    if r is None:
+        return False
+    hdr, out, total = r
+    if timer is not None:
+        torch.cuda.synchronize()
+        timer.add("encode", t0)
+    t0 = time.perf_counter()
+    f.write(hdr)
+    K = (total + D2H_CHUNK - 1) // D2H_CHUNK
+    pins = [torch.empty(min(D2H_CHUNK, max(1, total)), dtype=torch.uint8, pin_memory=True)
+            for _ in range(min(2, max(1, K)))]
+    evs = [torch.cuda.Event() for _ in pins]
+    cs = torch.cuda.Stream()
+    cs.wait_stream(torch.cuda.current_stream())
+
+    def issue(k):
+        a, b = k * D2H_CHUNK, min(total, (k + 1) * D2H_CHUNK)
+        with torch.cuda.stream(cs):
+            pins[k % 2][:b - a].copy_(out[a:b], non_blocking=True)
+            evs[k % 2].record(cs)
+
+    if K:
+        issue(0)
+    for k in range(K):
+        evs[k % 2].synchronize()
+        a, b = k * D2H_CHUNK, min(total, (k + 1) * D2H_CHUNK)
+        view = pins[k % 2][:b - a].numpy()
+        if k + 1 < K:
+            # the other buffer's previous piece was written at k - 1
+            issue(k + 1)
+        f.write(memoryview(view))
+    if timer is not None:
+        timer.add("d2h+write", t0)
+    return True
+
+
+def write_device(out_path: str, y, n: int, ch: int, sr: int, log=print, timer=None,
+                 device_encoder: bool = True):
     """FLAC PCM_24 of device samples y [n*ch], else the reference's WAV fallback
     at ``out_path.replace('.flac', '.wav')`` (src/process_tomatis.py:242-251).
     As in the reference, only a failure to *open* the FLAC output (the file or
     the encoder) falls back to WAV; an error while encoding or writing (a device
     error in the quantiser, a full disk) removes the partial file and raises.
-    Frame bytes are written by a writer thread while later segments encode;
-    the header goes over a placeholder at the end.  Returns (written_path, is_flac)."""
+    FLAC frames are encoded on the device (``tomatis_flacd_*``) and copied out
+    while the file is written; shapes the device encoder declines go through
+    the host encoder, whose frame bytes a writer thread writes while later
+    segments encode (the header over a placeholder at the end).  Both give the
+    same bytes.  Returns (written_path, is_flac)."""
     if audio_io.have_soundfile():
         return audio_io.write_with_fallback(out_path, y.cpu().numpy().reshape(n, ch), sr, log=log)
     import queue
@@ -269,6 +393,11 @@ def write_device(out_path: str, y, n: int, ch: int, sr: int, log=print, timer=No
         return wav_path, False
     try:
         with f:
+            if device_encoder and _write_device_frames(f, y, n, ch, sr, timer):
+                log("[OK] 输出格式: FLAC 24-bit")
+                return out_path, True
+            f.seek(0)
+            f.truncate()
             f.write(b"\0" * 42)
             q = queue.Queue(maxsize=4)
             err = []
@@ -330,5 +459,5 @@ def device_stream_set(x, n: int, ch: int, sr: int):
     return engine.StreamSet(x=x, offs=[0], lens=[n], ch=ch, sr=sr)
 
 
-__all__ = ["read_device", "write_device", "encode_flac_device", "requantize_device",
-           "device_stream_set", "Timer"]
+__all__ = ["read_device", "write_device", "encode_flac_device", "encode_flac_device_frames",
+           "requantize_device", "device_stream_set", "Timer"]
