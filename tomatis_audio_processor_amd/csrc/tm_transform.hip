@@ -203,49 +203,80 @@ constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141;
 template <int N> constexpr int kDppRowShl = 0x100 + N;
 template <int N> constexpr int kDppRowShr = 0x110 + N;
 
-// m*m of one sample, m = sqrt(mean over channels of x^2) (CH = 2: L + iR).
-// This unit compiles with -ffp-contract=fast, which lets the backend fuse any
-// multiply-add whatever the source pragmas: the squares go through opaque
-// copies so L^2 + R^2 stays two roundings, as numpy's frame**2 then sum.
+// a = mean over channels of x^2 for one sample (CH = 2: L + iR), as numpy's
+// frame**2 then mean(axis=1).  This unit compiles with -ffp-contract=fast,
+// which lets the backend fuse any multiply-add whatever the source pragmas: the
+// squares go through opaque copies so L^2 + R^2 stays two roundings.
 template <int CH>
-__device__ __forceinline__ float lv_msq(cf v) {
+__device__ __forceinline__ float lv_a(cf v) {
   if constexpr (CH == 2) {
     const float ll = opaque_f(v.x * v.x), rr = opaque_f(v.y * v.y);
-    const float m = sqrtf((ll + rr) * 0.5f);
-    return m * m;
+    return (ll + rr) * 0.5f;
   } else {
-    const float m = sqrtf(v.x * v.x);
-    return m * m;
+    return v.x * v.x;
   }
+}
+// m*m with m = sqrtf(a) correctly rounded, for a >= 2^-96, 0, +inf or NaN:
+// v_sqrt_f32 (<= 1 ulp) and one step to the neighbour whose residual says so
+// -- the expansion hipcc emits for sqrtf without its small-input scaling and
+// its zero / inf fix-up, which these inputs do not need (0: the residuals are
+// NaN / -0 and keep 0; +inf: NaN residuals keep +inf)
+__device__ __forceinline__ float lv_sq_fast(float a) {
+  const float s = __builtin_amdgcn_sqrtf(a);
+  const float sd = __int_as_float(__float_as_int(s) - 1);
+  const float su = __int_as_float(__float_as_int(s) + 1);
+  const float vd = __builtin_fmaf(-sd, s, a), vu = __builtin_fmaf(-su, s, a);
+  float m = vd <= 0.f ? sd : s;
+  m = vu > 0.f ? su : m;
+  return m * m;
 }
 
 // leaf sums of the hop block in the last SH registers of v; returns them in
-// lanes 8 l (l < LB).  scr: this sequence's LDS scratch (>= LB * kLvLS floats)
+// lanes 8 l (l < LB).  scr: this sequence's LDS scratch (>= LB * kLvLS floats).
+// A wave whose block holds no 0 < a < 2^-96 (anything but near-silent
+// non-zero samples below 2^-47) takes the short sqrt; otherwise sqrtf.
 template <int CH, int SH, int NRV>
 __device__ __forceinline__ float lv_leaves(const cf (&v)[NRV], float* scr, int L) {
   constexpr int LB = SH / 2;
+  float a[SH];
+  bool tiny = false;
 #pragma unroll
-  for (int j = 0; j < SH; ++j)
-    scr[(j >> 1) * kLvLS + (L & 7) * kLvCS + (L >> 3) + 8 * (j & 1)] = lv_msq<CH>(v[NRV - SH + j]);
+  for (int j = 0; j < SH; ++j) {
+    a[j] = lv_a<CH>(v[NRV - SH + j]);
+    tiny |= (a[j] > 0.f) & (a[j] < 0x1p-96f);
+  }
+  auto slot = [&](int j) -> float& {
+    return scr[(j >> 1) * kLvLS + (L & 7) * kLvCS + (L >> 3) + 8 * (j & 1)];
+  };
+  if (__builtin_amdgcn_ballot_w64(tiny) == 0) {
+#pragma unroll
+    for (int j = 0; j < SH; ++j) slot(j) = lv_sq_fast(a[j]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < SH; ++j) {
+      const float m = sqrtf(a[j]);
+      slot(j) = m * m;
+    }
+  }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const int leaf = min(L >> 3, LB - 1);
   const float4* p = reinterpret_cast<const float4*>(scr + leaf * kLvLS + (L & 7) * kLvCS);
   const float4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
-  float a = q0.x;
-  a = a + q0.y; a = a + q0.z; a = a + q0.w;
-  a = a + q1.x; a = a + q1.y; a = a + q1.z; a = a + q1.w;
-  a = a + q2.x; a = a + q2.y; a = a + q2.z; a = a + q2.w;
-  a = a + q3.x; a = a + q3.y; a = a + q3.z; a = a + q3.w;
-  a = a + dpp<kDppXor1>(a);        // lanes c, c^1: r0 + r1 ...
-  a = a + dpp<kDppXor2>(a);        // (r0 + r1) + (r2 + r3) in lanes 0..3
-  a = a + dpp<kDppHalfMirror>(a);  // lane 0: + ((r4 + r5) + (r6 + r7)) from lane 7
+  float a0 = q0.x;
+  a0 = a0 + q0.y; a0 = a0 + q0.z; a0 = a0 + q0.w;
+  a0 = a0 + q1.x; a0 = a0 + q1.y; a0 = a0 + q1.z; a0 = a0 + q1.w;
+  a0 = a0 + q2.x; a0 = a0 + q2.y; a0 = a0 + q2.z; a0 = a0 + q2.w;
+  a0 = a0 + q3.x; a0 = a0 + q3.y; a0 = a0 + q3.z; a0 = a0 + q3.w;
+  a0 = a0 + dpp<kDppXor1>(a0);        // lanes c, c^1: r0 + r1 ...
+  a0 = a0 + dpp<kDppXor2>(a0);        // (r0 + r1) + (r2 + r3) in lanes 0..3
+  a0 = a0 + dpp<kDppHalfMirror>(a0);  // lane 0: + ((r4 + r5) + (r6 + r7)) from lane 7
   // the scratch is reused by the next block / the FFT exchanges: reads done
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  return a;
+  return a0;
 }
 
 // window of the next frame: drop the oldest block's LB leaves, append the new
