@@ -56,6 +56,9 @@ def _assert_same(torch, pipe, ref):
     ("no_delay", 2, 30, 2, 44100, 512, 0.0, [1.0, 0.1]),
     ("long_delay", 1, 60, 2, 22050, 256, 2000.0, [0.7]),
     ("short", 4, 1, 2, 44100, 512, 250.0, [1.0, 0.5, 0.1, 1.0]),
+    # near-silent non-zero samples (mean square < 2^-96): the sqrtf branch
+    ("tiny", 3, 20, 2, 44100, 512, 250.0, [1e-18, 1.0, 3e-16]),
+    ("tiny_mono", 1, 20, 1, 44100, 256, 250.0, [1e-17]),
 ])
 def test_gated_bit_identical(case):
     torch, E = _engine()
