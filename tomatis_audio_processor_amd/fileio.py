@@ -115,10 +115,13 @@ def _read_flac_device(path, timer=None):
         x, n, ch, sr = _decode_flac_ranges(h, torch, buf, size, path, timer)
         del mv
     finally:
+        t1 = time.perf_counter()
         try:
             mm.close()
         except BufferError:  # an export is still alive: the map goes with it
             pass
+        if timer is not None:
+            timer.add("unmap", t1)
     return x, n, ch, sr
 
 
@@ -380,11 +383,14 @@ def write_device(out_path: str, y, n: int, ch: int, sr: int, log=print, timer=No
     import queue
     import threading
     h = _flac()
+    t_open = time.perf_counter()
     try:
         enc = C.c_void_p()
         _err(h.tomatis_flac_enc_open(ch, sr, 24, C.byref(enc)), "FLAC encoder")
         h.tomatis_flac_enc_close(enc)
         f = open(out_path, "wb")
+        if timer is not None:
+            timer.add("open", t_open)
     except Exception as e:
         log(f"[WARN] FLAC 写入失败: {e}")
         wav_path = out_path.replace(".flac", ".wav")
@@ -394,6 +400,10 @@ def write_device(out_path: str, y, n: int, ch: int, sr: int, log=print, timer=No
     try:
         with f:
             if device_encoder and _write_device_frames(f, y, n, ch, sr, timer):
+                t_close = time.perf_counter()
+                f.close()
+                if timer is not None:
+                    timer.add("close", t_close)
                 log("[OK] 输出格式: FLAC 24-bit")
                 return out_path, True
             f.seek(0)

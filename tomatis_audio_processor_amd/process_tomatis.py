@@ -52,12 +52,19 @@ def run_gate_path(in_path, out_path, *, xfade_ms=None, timer=None, **params):
     memory and streamed to HBM, PCM_24 quantised on the device and encoded
     while the next segment is copied back).  Returns (result, written, is_flac, N)."""
     from . import engine, fileio
+    import time
     import torch
     x, n, ch, sr = fileio.read_device(in_path, timer)
+    t0 = time.perf_counter()
     ss = fileio.device_stream_set(x, n, ch, sr)
     pipe = engine.GatePipeline(ss, xfade_ms=xfade_ms, **params)
+    if timer is not None:
+        timer.add("plan", t0)
+    t0 = time.perf_counter()
     res = pipe.run()
     torch.cuda.synchronize()
+    if timer is not None:
+        timer.add("process", t0)
     y = res.y[res.out_offs[0]:res.out_offs[0] + res.out_lens[0] * ch]
     written, is_flac = fileio.write_device(out_path, y, res.out_lens[0], ch, sr, timer=timer)
     return res, written, is_flac, n
