@@ -368,6 +368,32 @@ int tomatis_flacd_write(const int32_t* pcm, int64_t frames, int32_t ch, int32_t 
                         const void* ws, const int64_t* frame_off, uint8_t* out,
                         void* hip_stream);
 
+/* FLAC frames decoded on the device (row f1 ingest; src/process_tomatis.py:
+ * 225-235 read the input through libsndfile).  The grammar and checks of
+ * tomatis_flac_decode (include/tomatis_flac.h), for 1-2 channels and 4-24 bits
+ * (TOMATIS_E_UNSUPPORTED otherwise).  d: the file's bytes in device memory,
+ * 4-byte aligned, followed by >= 8 zero bytes; ch / bps from STREAMINFO.
+ *   tomatis_flacd_find: every byte position in [first, len) with a frame sync
+ *     code whose header parses and matches its CRC-8, appended (unordered) to
+ *     cand (int64 offsets, at most cap; *count = all found, device int32,
+ *     zeroed by the caller).
+ *   tomatis_flacd_scan: per candidate (sorted or not) info[4i..4i+3] = frame
+ *     bytes (0: no frame: a sub-frame, residual or CRC-16 check failed), first
+ *     sample (frame number x nominal for fixed-blocksize frames), block size,
+ *     blocking strategy bit.
+ *   tomatis_flacd_decode: the frames at byte offsets frames[0, nf) (verified,
+ *     chained: the caller checks that they tile the stream) into interleaved
+ *     int32 pcm (samples >= max_frames dropped); *err (device, zeroed by the
+ *     caller) != 0 if a frame failed to decode. */
+int tomatis_flacd_find(const uint8_t* d, int64_t len, int64_t first, int32_t ch, int32_t bps,
+                       int64_t* cand, int32_t cap, int32_t* count, void* hip_stream);
+int tomatis_flacd_scan(const uint8_t* d, int64_t len, const int64_t* cand, int32_t nc,
+                       int32_t ch, int32_t bps, int64_t nominal, int64_t* info,
+                       void* hip_stream);
+int tomatis_flacd_decode(const uint8_t* d, int64_t len, const int64_t* frames, int32_t nf,
+                         int32_t ch, int32_t bps, int64_t nominal, int32_t* pcm,
+                         int64_t max_frames, int32_t* err, void* hip_stream);
+
 /* max |x| over n floats as float bits (out zeroed by caller). */
 int tomatis_absmax(const float* x, int64_t n, uint32_t* out_bits, void* hip_stream);
 

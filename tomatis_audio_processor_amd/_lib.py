@@ -104,6 +104,12 @@ _SIGS = {
     "tomatis_flacd_workspace_bytes": (C.c_int64, [C.c_int64, C.c_int32]),
     "tomatis_flacd_plan": (C.c_int, [_P, C.c_int64, C.c_int32, C.c_int32, _P, _P, _P]),
     "tomatis_flacd_write": (C.c_int, [_P, C.c_int64, C.c_int32, C.c_int32, _P, _P, _P, _P]),
+    "tomatis_flacd_find": (C.c_int, [_P, C.c_int64, C.c_int64, C.c_int32, C.c_int32, _P,
+                                     C.c_int32, _P, _P]),
+    "tomatis_flacd_scan": (C.c_int, [_P, C.c_int64, _P, C.c_int32, C.c_int32, C.c_int32,
+                                     C.c_int64, _P, _P]),
+    "tomatis_flacd_decode": (C.c_int, [_P, C.c_int64, _P, C.c_int32, C.c_int32, C.c_int32,
+                                       C.c_int64, _P, C.c_int64, _P, _P]),
     "tomatis_stft_ola_gated_after_lookback": (C.c_int, [_P, _P, _P, C.c_int32, _P, _P, C.c_float,
                                                         _P, _P, _P]),
     "tomatis_ts_summary": (C.c_int, [_P, _P, C.c_int32, C.c_int32, _P, _P]),

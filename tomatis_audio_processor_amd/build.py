@@ -1,6 +1,6 @@
 """Build ``libtomatis_hip.so`` in-tree with hipcc for gfx950 (no cmake/ninja needed).
 
-Four translation units, compiled in parallel and linked into one C-ABI library:
+Six translation units, compiled in parallel and linked into one C-ABI library:
 
 * ``tm_kernels.hip``   levels, gate, limiter, plan and the ``extern "C"`` entry points;
 * ``tm_transform.hip`` the fused transform kernels (FMA contraction on;
@@ -8,7 +8,8 @@ Four translation units, compiled in parallel and linked into one C-ABI library:
   experiments — measured within 1 % of the default);
 * ``tm_analysis.hip``  analysis spectra for the validators / calibration tools
   (SURVEY.md §8 rows f3/f4);
-* ``tm_flacenc.hip``   FLAC frames encoded on the device (row f1's egress).
+* ``tm_flacenc.hip``   FLAC frames encoded on the device (row f1's egress);
+* ``tm_flacdec.hip``   FLAC frames decoded on the device (row f1's ingest).
 """
 from __future__ import annotations
 
@@ -30,6 +31,7 @@ UNITS = {  # source -> extra flags
                         (["-mllvm", f"-amdgpu-sched-strategy={SCHED}"] if SCHED else []),
     "tm_analysis.hip": [],
     "tm_flacenc.hip": [],
+    "tm_flacdec.hip": [],
 }
 DEPS = [os.path.join(CSRC, f) for f in (*UNITS, "tm_common.h", "tm_fft.h", "tm_shared.h",
                                         "tm_lds_fft.h", "tm_host_dsp.h", "tm_gate.h")] + \

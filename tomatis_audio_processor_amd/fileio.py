@@ -112,7 +112,11 @@ def _read_flac_device(path, timer=None):
         buf, size = mv.ctypes.data + skip, len(mm) - skip
         if timer is not None:
             timer.add("read", t0)
-        x, n, ch, sr = _decode_flac_ranges(h, torch, buf, size, path, timer)
+        r = _decode_flac_on_device(h, torch, mv[skip:], buf, size, timer)
+        if r is None:
+            x, n, ch, sr = _decode_flac_ranges(h, torch, buf, size, path, timer)
+        else:
+            x, n, ch, sr = r
         del mv
     finally:
         t1 = time.perf_counter()
@@ -123,6 +127,106 @@ def _read_flac_device(path, timer=None):
         if timer is not None:
             timer.add("unmap", t1)
     return x, n, ch, sr
+
+
+UP_PARTS = 8                 # host threads copying the mapped file into page-locked memory
+# k_fdd_scan reports frame number x this for fixed-blocksize frames; a power of
+# two above any block size, so the frame number comes back exactly
+FLAC_NOMINAL_GUESS = 1 << 20
+
+
+def _decode_flac_on_device(h, torch, src, buf, size, timer=None):
+    """The FLAC stream src (uint8 numpy view of the mapped file, at address buf)
+    decoded on the device (tomatis_flacd_*): the bytes go up through a
+    page-locked block (host threads copy slices of the mapping, each slice DMA'd
+    as soon as it is in), candidate frames are found and verified there, and
+    the verified frames must tile the stream -- first frame at the first frame
+    offset, each next one where the previous ended, consecutive samples to the
+    STREAMINFO total, the last one ending at the end of the file.  Returns
+    (x float32 [n*ch], n, ch, sr), or None for the host decoder (other shapes,
+    a stream of unknown length, trailing bytes, anything that does not chain)."""
+    import concurrent.futures as cf
+    L = lib()
+    sr_, ch_, bps_, n_ = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int64()
+    if h.tomatis_flac_info(buf, size, C.byref(sr_), C.byref(ch_), C.byref(bps_), C.byref(n_)):
+        return None
+    sr, ch, bps, n = sr_.value, ch_.value, bps_.value, n_.value
+    if not (1 <= ch <= 2 and 4 <= bps <= 24) or n <= 0:
+        return None
+    first = int(h.tomatis_flac_first_frame(buf, size))
+    if first < 0:
+        return None
+    t0 = time.perf_counter()
+    hs = stream_handle()
+    dev = torch.empty((size + 8 + 3) // 4 * 4, dtype=torch.uint8, device="cuda")
+    dev[size:].zero_()
+    pin = torch.empty(max(1, size), dtype=torch.uint8, pin_memory=True)
+    pin_np = pin.numpy()
+    cs = torch.cuda.Stream()
+    cs.wait_stream(torch.cuda.current_stream())
+    edges = np.linspace(0, size, UP_PARTS + 1).astype(np.int64)
+
+    def part(k):
+        a, b = int(edges[k]), int(edges[k + 1])
+        np.copyto(pin_np[a:b], src[a:b])
+        return k
+
+    with cf.ThreadPoolExecutor(max_workers=UP_PARTS) as ex:
+        for k in ex.map(part, range(UP_PARTS)):   # in order: DMA slice k once it is in
+            a, b = int(edges[k]), int(edges[k + 1])
+            if b > a:
+                with torch.cuda.stream(cs):
+                    dev[a:b].copy_(pin[a:b], non_blocking=True)
+    torch.cuda.current_stream().wait_stream(cs)
+    if timer is not None:
+        torch.cuda.synchronize()
+        timer.add("upload", t0)
+    t0 = time.perf_counter()
+    cap = n // 16 + 4096
+    cand = torch.empty(cap, dtype=torch.int64, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    check(L.tomatis_flacd_find(ptr(dev), size, first, ch, bps, ptr(cand), cap, ptr(cnt), hs),
+          "flacd_find")
+    nc = int(cnt.item())
+    if nc == 0 or nc > cap:
+        return None
+    cand = torch.sort(cand[:nc]).values
+    info = torch.empty(4 * nc, dtype=torch.int64, device="cuda")
+    check(L.tomatis_flacd_scan(ptr(dev), size, ptr(cand), nc, ch, bps, FLAC_NOMINAL_GUESS, ptr(info),
+                               hs), "flacd_scan")
+    inf = info.view(nc, 4).cpu().numpy()
+    offs = cand.cpu().numpy()
+    ok = inf[:, 0] > 0
+    fo, fb, fs, fn, fv = offs[ok], inf[ok, 0], inf[ok, 1], inf[ok, 2], inf[ok, 3]
+    if len(fo) == 0 or not (np.all(fv == fv[0])):
+        return None
+    # one fixed block size (the nominal one of every frame but the last) or
+    # the coded sample numbers; the scan took frame numbers x the guess
+    nominal = int(fn[0])
+    chain = (fo[0] == first and np.array_equal(fo[1:], fo[:-1] + fb[:-1]) and
+             int(fo[-1] + fb[-1]) == size)
+    if not chain:
+        return None
+    fixed = fv[0] == 0
+    if fixed and not (np.all(fn[:-1] == nominal) and fn[-1] <= nominal):
+        return None
+    start = fs // FLAC_NOMINAL_GUESS * nominal if fixed else fs
+    if not (start[0] == 0 and np.array_equal(start[1:], start[:-1] + fn[:-1]) and
+            int(start[-1] + fn[-1]) >= n):
+        return None
+    frames = torch.from_numpy(np.ascontiguousarray(fo)).to("cuda")
+    pcm = torch.empty(max(1, n * ch), dtype=torch.int32, device="cuda")
+    err = torch.zeros(1, dtype=torch.int32, device="cuda")
+    check(L.tomatis_flacd_decode(ptr(dev), size, ptr(frames), len(fo), ch, bps,
+                                 nominal if fixed else 0, ptr(pcm), n, ptr(err), hs),
+          "flacd_decode")
+    x = torch.empty(max(1, n * ch), dtype=torch.float32, device="cuda")
+    check(L.tomatis_pcm_to_float(ptr(pcm), n * ch, bps, ptr(x), hs), "pcm_to_float")
+    if int(err.item()):
+        return None
+    if timer is not None:
+        timer.add("decode", t0)
+    return x[:n * ch], n, ch, sr
 
 
 def _decode_flac_ranges(h, torch, buf, size, path, timer):
