@@ -75,6 +75,26 @@ def test_gated_bit_identical(case):
     _assert_same(torch, pipe, ref)
 
 
+def test_gated_digital_silence():
+    """Exact zeros (digital silence) inside interior runs, next to loud and
+    near-silent stretches: hop blocks holding a zero, a sub-2^-47 sample or
+    an inf-free loud block take different sqrt forms in the fused levels
+    (rsq form only for finite mean squares >= 2^-96); all must equal the
+    two-pass chain bit for bit."""
+    torch, E = _engine()
+    sr, n = 44100, 44100 * 30 + 77
+    ss = E.StreamSet.synthetic(2, n, 2, sr, seed0=321)
+    for i in range(2):
+        o = ss.offs[i]
+        a, b = o + 2 * (sr * 5 + 100 * (i + 1)), o + 2 * (sr * 9)
+        ss.x[a:b] = 0.0                               # silence
+        ss.x[b:b + 2 * sr] *= 1e-20                   # near-silent (mean square < 2^-96)
+        ss.x[o + 2 * sr * 15:o + 2 * sr * 15 + 2 * 700:7] = 0.0  # scattered zeros in loud audio
+    pipe, ref = _pair(E, ss, gate_ui=50, n_fft=2048, hop=512)
+    assert pipe.gated_used and pipe.gate_fallbacks == 0
+    _assert_same(torch, pipe, ref)
+
+
 def test_gated_ragged_and_two_rounds():
     """Ragged stream lengths (edge runs, streams shorter than a frame) and the
     two-round fused limiter under the fused gate."""

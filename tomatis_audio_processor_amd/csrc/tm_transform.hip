@@ -203,58 +203,82 @@ constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141;
 template <int N> constexpr int kDppRowShl = 0x100 + N;
 template <int N> constexpr int kDppRowShr = 0x110 + N;
 
+// a value the compiler may not look through (no instruction: the empty asm
+// only ends FMA contraction and value tracking at this point)
+__device__ __forceinline__ float lv_opq(float v) {
+  __asm__ volatile("" : "+v"(v));
+  return v;
+}
 // a = mean over channels of x^2 for one sample (CH = 2: L + iR), as numpy's
 // frame**2 then mean(axis=1).  This unit compiles with -ffp-contract=fast,
 // which lets the backend fuse any multiply-add whatever the source pragmas: the
-// squares go through opaque copies so L^2 + R^2 stays two roundings.
+// squares pass through lv_opq so L^2 + R^2 stays two roundings.
 template <int CH>
 __device__ __forceinline__ float lv_a(cf v) {
   if constexpr (CH == 2) {
-    const float ll = opaque_f(v.x * v.x), rr = opaque_f(v.y * v.y);
+    const float ll = lv_opq(v.x * v.x), rr = lv_opq(v.y * v.y);
     return (ll + rr) * 0.5f;
   } else {
     return v.x * v.x;
   }
 }
-// m*m with m = sqrtf(a) correctly rounded, for a >= 2^-96, 0, +inf or NaN:
-// v_sqrt_f32 (<= 1 ulp) and one step to the neighbour whose residual says so
-// -- the expansion hipcc emits for sqrtf without its small-input scaling and
-// its zero / inf fix-up, which these inputs do not need (0: the residuals are
-// NaN / -0 and keep 0; +inf: NaN residuals keep +inf)
-__device__ __forceinline__ float lv_sq_fast(float a) {
+// sqrtf(a) correctly rounded for a >= 2^-96, 0, +inf or NaN: v_sqrt_f32
+// (<= 1 ulp) and one step to the neighbour whose residual says so -- the
+// expansion hipcc emits for sqrtf without its small-input scaling and its
+// zero / inf fix-up, which these inputs do not need (0: the residuals are NaN /
+// -0 and keep 0; +inf: NaN residuals keep +inf)
+__device__ __forceinline__ float lv_sqrt_fast(float a) {
   const float s = __builtin_amdgcn_sqrtf(a);
   const float sd = __int_as_float(__float_as_int(s) - 1);
   const float su = __int_as_float(__float_as_int(s) + 1);
   const float vd = __builtin_fmaf(-sd, s, a), vu = __builtin_fmaf(-su, s, a);
   float m = vd <= 0.f ? sd : s;
   m = vu > 0.f ? su : m;
-  return m * m;
+  return m;
 }
+// any a >= 0 (or NaN): below 2^-96 through a x 2^64 (sqrt scales by exactly
+// 2^32, no rounding moves: every m here is normal)
+__device__ __forceinline__ float lv_sqrt_any(float a) {
+  const bool sc = a < 0x1p-96f;
+  const float m = lv_sqrt_fast(sc ? a * 0x1p64f : a);
+  return sc ? m * 0x1p-32f : m;
+}
+// bits(a) - 1 for the tiny test: 0 < a < 2^-96 <=> bits(a) - 1 < bits(2^-96) - 1
+// (a >= +0 or NaN here: a sum of squares).  (A v_rsq_f32 form, s = a y,
+// m = s + (a - s^2) y / 2, is correctly rounded on every float in [2^-96, inf)
+// -- checked exhaustively on gfx950, tools/sqrt_probe.hip -- and two VALU
+// cheaper per sample, but it pushed the frame loop into scratch spills and
+// measured slower; not used.)
+constexpr uint32_t kLvTiny = 0x0f800000u - 1u;
 
 // leaf sums of the hop block in the last SH registers of v; returns them in
 // lanes 8 l (l < LB).  scr: this sequence's LDS scratch (>= LB * kLvLS floats).
 // A wave whose block holds no 0 < a < 2^-96 (anything but near-silent
-// non-zero samples below 2^-47) takes the short sqrt; otherwise sqrtf.
+// non-zero samples below 2^-47) takes the short sqrt; otherwise the same
+// neighbour-residual form with the small-input scaling.
 template <int CH, int SH, int NRV>
 __device__ __forceinline__ float lv_leaves(const cf (&v)[NRV], float* scr, int L) {
   constexpr int LB = SH / 2;
   float a[SH];
-  bool tiny = false;
+  uint32_t umin = 0xffffffffu;
 #pragma unroll
   for (int j = 0; j < SH; ++j) {
     a[j] = lv_a<CH>(v[NRV - SH + j]);
-    tiny |= (a[j] > 0.f) & (a[j] < 0x1p-96f);
+    umin = min(umin, __float_as_uint(a[j]) - 1u);
   }
   auto slot = [&](int j) -> float& {
     return scr[(j >> 1) * kLvLS + (L & 7) * kLvCS + (L >> 3) + 8 * (j & 1)];
   };
-  if (__builtin_amdgcn_ballot_w64(tiny) == 0) {
+  if (__builtin_amdgcn_ballot_w64(umin < kLvTiny) == 0) {
 #pragma unroll
-    for (int j = 0; j < SH; ++j) slot(j) = lv_sq_fast(a[j]);
+    for (int j = 0; j < SH; ++j) {
+      const float m = lv_sqrt_fast(a[j]);
+      slot(j) = m * m;
+    }
   } else {
 #pragma unroll
     for (int j = 0; j < SH; ++j) {
-      const float m = sqrtf(a[j]);
+      const float m = lv_sqrt_any(a[j]);
       slot(j) = m * m;
     }
   }
@@ -303,7 +327,7 @@ __device__ __forceinline__ float lv_frame_r(float lw) {
   t = t + dpp<kDppRowShl<8>>(t);
   const float tot = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(t)));
   const float mean = tot * (1.0f / 2048.0f);  // exact (numpy divides by n = 2^11)
-  return sqrtf(opaque_f(mean) + kEps32);
+  return lv_sqrt_fast(lv_opq(mean) + kEps32);  // mean + EPS >= 1e-12 (or NaN / inf)
 }
 
 // read-only (for the kernel's lifetime) data through the scalar cache: a
@@ -425,12 +449,14 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   auto gate_frame = [&](const cf (&fr)[NR], int64_t k, bool emit) -> uint32_t {
     lw = lv_window<SH, true>(lw, lv_leaves<CH, SH, NR>(fr, lscr, L));
     const float r = lv_frame_r(lw);
-    uint8_t pr;
+    // r is wave-uniform: its bits through readfirstlane keep the predicate and
+    // the automaton in SGPRs / SALU
+    const uint32_t b = __builtin_amdgcn_readfirstlane(__float_as_uint(r));
+    uint32_t pr;
     if (g_exc) {
-      pr = gate_pred(r, A.st[opaque(R.s)]);
+      pr = __builtin_amdgcn_readfirstlane(gate_pred(__uint_as_float(b), A.st[opaque(R.s)]));
     } else {
-      const uint32_t b = __float_as_uint(r);
-      pr = (r != r) ? 0 : (uint8_t)((b >= g_on ? 1 : 0) | (b <= g_off ? 2 : 0));
+      pr = ((b & 0x7fffffffu) > 0x7f800000u) ? 0u : ((b >= g_on ? 1u : 0u) | (b <= g_off ? 2u : 0u));
     }
     gid = gate_step(gid, pr, A.gate_D);
     const bool c2 = gid == A.gate_D + 1;
