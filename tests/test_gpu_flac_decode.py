@@ -71,6 +71,34 @@ def test_device_decode_independent_writer(tmp_path, assign):
     _check(torch, audio_io, fileio, tmp_path, blob, f"indep_{assign}")
 
 
+def _set_total(blob, n):
+    """STREAMINFO's 36-bit total-samples field (bytes 18..25 hold sample rate,
+    channels, bits and the total) set to n."""
+    b = bytearray(blob)
+    v = int.from_bytes(b[18:26], "big")
+    b[18:26] = ((v & ~((1 << 36) - 1)) | n).to_bytes(8, "big")
+    return bytes(b)
+
+
+@pytest.mark.parametrize("total", [700, 456, 300])
+def test_device_decode_short_total_falls_back(tmp_path, total):
+    """STREAMINFO declaring fewer samples than the LPC frames hold: the frames
+    past the total (or straddling it) cannot be decoded whole into the PCM
+    buffer, so the device declines (no read outside the frames' written
+    samples) and the host decoder's truncated result is returned."""
+    torch, audio_io, fileio = _mods()
+    from tests.test_flac_codec import py_flac
+    rng = np.random.default_rng(5)
+    frames = []
+    for n in (256, 200, 256, 128):
+        t = np.arange(n)
+        base = (np.sin(t * 0.05) * 3e6).astype(np.int64)
+        frames.append(np.stack([base + rng.integers(-50, 50, n),
+                                base // 2 + rng.integers(-50, 50, n)], 1))
+    blob = _set_total(py_flac(frames, 48000, 24, 9), total)
+    _check(torch, audio_io, fileio, tmp_path, blob, f"short_{total}", expect_device=False)
+
+
 def test_device_decode_trailing_tag_falls_back(tmp_path):
     torch, audio_io, fileio = _mods()
     rng = np.random.default_rng(3)

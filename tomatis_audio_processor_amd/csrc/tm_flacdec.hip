@@ -203,6 +203,11 @@ __device__ bool walk_subframes(BR& r, const FHdr& h, int32_t* out, int ostride, 
       const bool lpc = (type & 0x20) != 0;
       const int order = lpc ? (type & 0x1F) + 1 : (type & 7);
       if ((!lpc && order > 4) || order > n) return false;
+      // LPC predicts from its own output read back: only a frame that lies
+      // wholly inside the PCM buffer (take == n) may be decoded here; one that
+      // reaches past the stream's sample count goes to the host decoder (no
+      // read outside the frame's written samples)
+      if (DEC && lpc && take < n) return false;
       // warm-up samples (unshifted values kept for the prediction)
       int32_t hist[4] = {0, 0, 0, 0};  // FIXED: last samples, hist[0] newest
       for (int i = 0; i < order; ++i) {
@@ -269,7 +274,6 @@ __device__ bool walk_subframes(BR& r, const FHdr& h, int32_t* out, int ostride, 
               hist[0] = s;
             }
             if (i < take) o[(int64_t)i * ostride] = s;
-            else if (lpc) return false;  // LPC reads back its history: keep it whole
           }
         }
         if (r.bad) return false;
