@@ -124,3 +124,49 @@ def test_device_decode_c2_file(tmp_path):
                              float(1 << (bps - 1))).astype(np.float32)).cuda()
     assert torch.equal(x[:n * 2], want)
 
+
+
+def test_device_decode_corrupted_bytes(tmp_path):
+    """Single-byte corruptions anywhere in a stream (metadata, frame headers,
+    subframe headers, residuals, CRCs): the device kernels must stay inside the
+    file's bytes, and the device read must return what the host decoder
+    returns (or raise what it raises) — a corrupted frame fails its CRC-8 /
+    CRC-16 or breaks the frame chain, and the read goes to the host decoder."""
+    torch, audio_io, fileio = _mods()
+    from tests.test_gpu_flac_device import _signals
+    rng = np.random.default_rng(77)
+    from tests.test_flac_codec import py_flac
+    x = _signals(rng, 4096 * 3 + 301, 24)["tone_noise"]
+    own = audio_io.flac_encode_int(np.ascontiguousarray(x), 44100, 24)
+    frames = []
+    for n in (256, 200, 256, 128):  # LPC, escapes, Rice2, wasted bits
+        t = np.arange(n)
+        base = (np.sin(t * 0.05) * 3e6).astype(np.int64)
+        L = base + rng.integers(-50, 50, n)
+        frames.append(np.stack([L, L - 4 * ((L - base // 2) // 4)], 1))
+    indep = py_flac(frames, 48000, 24, 10)
+    p = tmp_path / "fz.flac"
+    for t in range(160):
+        blob = own if t % 2 else indep
+        b = bytearray(blob)
+        pos = int(rng.integers(0, len(b))) if t % 4 else int(rng.integers(0, min(len(b), 200)))
+        b[pos] ^= int(rng.integers(1, 256))
+        p.write_bytes(bytes(b))
+        try:
+            ref, sr2, bps = audio_io.flac_decode_int(bytes(b))
+            ref_err = None
+        except Exception as e:  # noqa: BLE001 - the host's verdict is the reference
+            ref_err = type(e)
+        try:
+            got, n, ch, sr = fileio.read_device(str(p), fileio.Timer())
+            got_err = None
+        except Exception as e:  # noqa: BLE001
+            got_err = type(e)
+        torch.cuda.synchronize()
+        if ref_err is not None:
+            assert got_err is not None, (t, pos)
+            continue
+        assert got_err is None, (t, pos, got_err)
+        want = (ref.astype(np.float64) / float(1 << (bps - 1))).astype(np.float32)
+        assert (n, ch) == ref.shape, (t, pos)
+        assert np.array_equal(got[:n * ch].cpu().numpy().reshape(n, ch), want), (t, pos)

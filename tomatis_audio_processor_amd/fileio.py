@@ -249,18 +249,28 @@ def _decode_flac_ranges(h, torch, buf, size, path, timer):
     got = 0
     t0 = time.perf_counter()
     for k in range(IN_RANGES):
-        _err(h.tomatis_flac_decode_bytes(buf, size, int(edges[k]), int(edges[k + 1]),
-                                         pin.data_ptr(), n, C.byref(s_lo), C.byref(s_hi)),
-             "FLAC decode failed")
+        if h.tomatis_flac_decode_bytes(buf, size, int(edges[k]), int(edges[k + 1]),
+                                       pin.data_ptr(), n, C.byref(s_lo), C.byref(s_hi)):
+            got = -1   # a damaged range: the whole-buffer decoder decides
+            break
         a, b = s_lo.value, s_hi.value
         if b > a:
-            if a != got:
-                raise audio_io.AudioFormatError(f"{path}: FLAC frames out of order / missing")
+            if a != got:   # frames missing / out of order: the whole-buffer decoder decides
+                got = -1
+                break
             with torch.cuda.stream(cs):   # DMA while the next range decodes
                 dev[a * ch:b * ch].copy_(pin[a * ch:b * ch], non_blocking=True)
             got = b
     if got != n:
-        raise audio_io.AudioFormatError(f"{path}: decoded {got} of {n} frames")
+        # a gap, or fewer samples than STREAMINFO's total: a truncated stream
+        # (the whole-buffer decoder returns the frames it holds) or a damaged
+        # frame (it raises) -- let it decide, with its result
+        cs.synchronize()
+        got_ = C.c_int64()
+        _err(h.tomatis_flac_decode(buf, size, pin.data_ptr(), n, C.byref(got_)),
+             "FLAC decode failed")
+        n = got_.value
+        dev[:n * ch].copy_(pin[:n * ch])
     torch.cuda.current_stream().wait_stream(cs)
     x = torch.empty(max(1, n * ch), dtype=torch.float32, device="cuda")
     check(lib().tomatis_pcm_to_float(ptr(dev), n * ch, bps, ptr(x), stream_handle()),
