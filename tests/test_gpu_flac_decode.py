@@ -2,7 +2,7 @@
 the file path; the reference reads its input through libsndfile,
 src/process_tomatis.py:225-235) against the host decoder (csrc/tm_flac.cpp):
 the same integers.  Streams from this build's encoder (every subframe kind
-and stereo assignment it picks, 8-24 bits, mono / stereo, short last blocks)
+and stereo assignment it picks, 4-24 bits, mono / stereo, short last blocks)
 and from the independent Python writer of test_flac_codec.py (LPC subframes,
 escape partitions, Rice2, wasted bits, side/right and mid/side, variable
 block size, 16-bit sample-rate headers).  A stream with trailing non-audio
@@ -41,7 +41,7 @@ def _check(torch, audio_io, fileio, tmp_path, blob, name, expect_device=True):
     assert np.array_equal(got, want), name
 
 
-@pytest.mark.parametrize("bps", [24, 16, 8])
+@pytest.mark.parametrize("bps", [24, 20, 16, 12, 8, 4])
 def test_device_decode_own_encoder(tmp_path, bps):
     torch, audio_io, fileio = _mods()
     from tests.test_gpu_flac_device import _signals
