@@ -383,8 +383,9 @@ int tomatis_flacd_write(const int32_t* pcm, int64_t frames, int32_t ch, int32_t 
  *     blocking strategy bit.
  *   tomatis_flacd_decode: the frames at byte offsets frames[0, nf) (verified,
  *     chained: the caller checks that they tile the stream) into interleaved
- *     int32 pcm (samples >= max_frames dropped); *err (device, zeroed by the
- *     caller) != 0 if a frame failed to decode. */
+ *     int32 pcm (samples >= max_frames dropped; an LPC frame reaching past
+ *     max_frames is not decoded: it predicts from its own output); *err
+ *     (device, zeroed by the caller) != 0 if a frame was not decoded. */
 int tomatis_flacd_find(const uint8_t* d, int64_t len, int64_t first, int32_t ch, int32_t bps,
                        int64_t* cand, int32_t cap, int32_t* count, void* hip_stream);
 int tomatis_flacd_scan(const uint8_t* d, int64_t len, const int64_t* cand, int32_t nc,
