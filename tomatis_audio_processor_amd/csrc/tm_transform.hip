@@ -199,7 +199,7 @@ template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, true));
 }
-constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141;
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141, kDppRowMirror = 0x140;
 template <int N> constexpr int kDppRowShl = 0x100 + N;
 template <int N> constexpr int kDppRowShr = 0x110 + N;
 
@@ -1019,13 +1019,34 @@ __global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restri
     for (int j = 0; j < SH; ++j)  // negative / past-the-end positions: out of range -> 0
       dst[j] = bload<CH>(rx, (int)(uint32_t)((p0 + 64 * j) * (CH * 4)), 0);
   };
+  // block energy (sum of the channel-mean squares) for the fast walk
+  auto block_energy = [&](const cf (&b)[SH]) -> float {
+    float e = 0.f;
+#pragma unroll
+    for (int q = 0; q < SH; ++q) e += CH == 2 ? (b[q].x * b[q].x + b[q].y * b[q].y) * 0.5f : b[q].x * b[q].x;
+    // wave sum, any order (DPP within 16-lane rows, then the 4 row sums)
+    e += dpp<kDppXor1>(e);
+    e += dpp<kDppXor2>(e);
+    e += dpp<kDppHalfMirror>(e);
+    e += dpp<kDppRowMirror>(e);
+    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e), 0));
+    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e), 16));
+    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e), 32));
+    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e), 48));
+    return (r0 + r1) + (r2 + r3);
+  };
   // window of frame kf - 1: blocks kf - 1 .. kf + NB - 2
   float lw = 0.f;
+  float eb[NB];  // fast walk: energies of the current frame's blocks, eb[0] the earliest
+  {
+    cf b[NB][SH];
 #pragma unroll
-  for (int i = 0; i < NB; ++i) {
-    cf b[SH];
-    load_block(kf - 1 + i, b);
-    lw = lv_window<SH, true>(lw, lv_leaves<CH, SH, SH>(b, scr, L));
+    for (int i = 0; i < NB; ++i) load_block(kf - 1 + i, b[i]);  // all loads in flight at once
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      eb[i] = block_energy(b[i]);
+      lw = lv_window<SH, true>(lw, lv_leaves<CH, SH, SH>(b[i], scr, L));
+    }
   }
   if (L < 16) win[(int64_t)run * 16 + L] = lw;
   int id = 0;
@@ -1035,7 +1056,70 @@ __global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restri
     int a_id = 0, on_run = 0, n = 0;
     cf bq[PFD][SH];              // blocks j - 1 - u, prefetched
     sfor<0, PFD>([&](auto uu) { load_block(j - 1 - decltype(uu)::value, bq[decltype(uu)::value]); });
-    bool more = true;
+    // Fast walk: the predicate of each frame from an approximate r (block
+    // energies summed in any order: within ~1e-5 relative of numpy's pairwise
+    // r) decided only when r is more than 0.1 % away from both thresholds.  A
+    // frame closer to a threshold (or a NaN, or a stream with exception lists)
+    // ends it, and the exact walk below recomputes the look-back from kf - 1.
+    bool exact = (S.n_on_exc | S.n_off_exc) != 0;
+    if (!exact) {
+      const float t_on = __uint_as_float(S.on_bits), t_off = __uint_as_float(S.off_bits);
+      constexpr float kM = 1e-3f;
+      bool go = true;
+      while (go) {
+        sfor<0, PFD>([&](auto uu) {
+          constexpr int u = decltype(uu)::value;
+          if (go) {
+            float es = 0.f;
+#pragma unroll
+            for (int i = 0; i < NB; ++i) es += eb[i];
+            const float ra = sqrtf(es * (1.0f / 2048.0f) + kEps32);
+            const bool on_s = ra >= t_on * (1.f + kM), non_s = ra < t_on * (1.f - kM);
+            const bool off_s = ra <= t_off * (1.f - kM), noff_s = ra > t_off * (1.f + kM);
+            if (!(on_s || non_s) || !(off_s || noff_s)) {
+              exact = true;  // too close to call
+              go = false;
+            } else {
+              const uint8_t pr = (uint8_t)((on_s ? 1 : 0) | (off_s ? 2 : 0));
+              if (L == 0) prs[n] = pr;
+              ++n;
+              on_run = (on_s && !off_s) ? on_run + 1 : 0;
+              if (!on_s && off_s) {
+                a_k = j;
+                a_id = 0;
+                go = false;
+              } else if (on_run == D + 1) {
+                a_k = j + D;
+                a_id = D + 1;
+                go = false;
+              } else if (j == 0) {
+                a_k = -1;
+                a_id = 0;
+                go = false;
+              } else if (n >= kGateLookback) {
+                exact = true;  // let the exact walk decide (and flag) this run
+                go = false;
+              } else {
+#pragma unroll
+                for (int i = NB - 1; i > 0; --i) eb[i] = eb[i - 1];
+                eb[0] = block_energy(bq[u]);
+                load_block(j - 1 - PFD, bq[u]);
+                --j;
+              }
+            }
+          }
+        });
+      }
+      if (exact) {  // restart from frame kf - 1
+        j = kf - 1;
+        a_k = -2;
+        a_id = 0;
+        on_run = 0;
+        n = 0;
+        sfor<0, PFD>([&](auto uu) { load_block(j - 1 - decltype(uu)::value, bq[decltype(uu)::value]); });
+      }
+    }
+    bool more = exact;
     while (more) {
       sfor<0, PFD>([&](auto uu) {
         constexpr int u = decltype(uu)::value;
