@@ -77,10 +77,11 @@ def test_gated_bit_identical(case):
 
 def test_gated_digital_silence():
     """Exact zeros (digital silence) inside interior runs, next to loud and
-    near-silent stretches: hop blocks holding a zero, a sub-2^-47 sample or
-    an inf-free loud block take different sqrt forms in the fused levels
-    (rsq form only for finite mean squares >= 2^-96); all must equal the
-    two-pass chain bit for bit."""
+    near-silent stretches: hop blocks of zeros and loud samples take the short
+    correctly rounded sqrt, blocks holding a near-silent sample (mean square
+    below 2^-96) the scaled form; the approximate look-back decides the loud
+    and silent frames and hands near-threshold ones to the exact walk.  All
+    must equal the two-pass chain bit for bit."""
     torch, E = _engine()
     sr, n = 44100, 44100 * 30 + 77
     ss = E.StreamSet.synthetic(2, n, 2, sr, seed0=321)
@@ -183,6 +184,19 @@ def test_gated_full_size_c2():
     sr = 44100
     n = 3600 * sr
     ss = E.StreamSet.synthetic(1, n, 2, sr, seed0=1000)
+    pipe, ref = _pair(E, ss, gate_ui=50, n_fft=2048, hop=512)
+    assert pipe.gated_used and pipe.gate_fallbacks == 0
+    _assert_same(torch, pipe, ref)
+
+
+def test_gated_full_size_c4():
+    """BASELINE C4 as benched per GPU (64 x 5 min stereo 48 kHz, seeds as
+    bench.py): the fused pass equals the two-pass chain bit for bit on every
+    stream (r, states, chunk peaks, output)."""
+    torch, E = _engine()
+    sr = 48000
+    n = 300 * sr
+    ss = E.StreamSet.synthetic(64, n, 2, sr, seed0=1000)
     pipe, ref = _pair(E, ss, gate_ui=50, n_fft=2048, hop=512)
     assert pipe.gated_used and pipe.gate_fallbacks == 0
     _assert_same(torch, pipe, ref)
