@@ -200,3 +200,33 @@ def test_gated_full_size_c4():
     pipe, ref = _pair(E, ss, gate_ui=50, n_fft=2048, hop=512)
     assert pipe.gated_used and pipe.gate_fallbacks == 0
     _assert_same(torch, pipe, ref)
+
+
+def test_gated_level_sweeps_through_thresholds():
+    """Levels that sweep through the hysteresis band with short plateaus at
+    each threshold (quiet -> up through both thresholds -> loud -> down, three
+    times): the plateau frames sit within 0.1 % of a threshold, where the
+    approximate look-back declines and the exact walk takes over; every run
+    still resolves, and the fused pass equals the two-pass chain bit for bit."""
+    torch, E = _engine()
+    sr, hop = 44100, 512
+    probe = E.GatePipeline(E.StreamSet.synthetic(1, sr, 2, sr, seed0=1), gate_ui=50,
+                           n_fft=2048, hop=hop)
+    ton, toff = probe.Ton, probe.Toff   # level thresholds (dB) of this gate setting
+    del probe
+    segs = []
+    for _ in range(3):
+        # plateaus at each threshold (0.25 s, fewer than up-delay + 1 frames)
+        for secs, d0, d1 in ((1.0, -60, -60), (1.0, -47, toff), (0.25, toff, toff),
+                             (0.5, toff, ton), (0.25, ton, ton), (1.0, ton, -33),
+                             (3.0, -20, -20), (2.0, -35, -45)):
+            m = int(secs * sr)
+            segs.append(np.linspace(d0, d1, m))
+    db = np.concatenate(segs)
+    t = np.arange(len(db)) / sr
+    s = (np.sqrt(2.0) * 10.0 ** (db / 20.0) * np.sin(2 * np.pi * 1000.0 * t)).astype(np.float32)
+    x = np.stack([s, s], 1)
+    ss = E.StreamSet.from_arrays([x, synth_stream(12, len(s), 2, sr)], sr)
+    pipe, ref = _pair(E, ss, gate_ui=50, n_fft=2048, hop=hop)
+    assert pipe.gated_used and pipe.gate_fallbacks == 0
+    _assert_same(torch, pipe, ref)
