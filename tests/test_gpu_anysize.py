@@ -86,7 +86,7 @@ def test_adaptive_quiet_f64_8192():
     assert float(res.extra["thresholds"].cpu().numpy()[0]) == ref["threshold"]
 
 
-@pytest.mark.parametrize("secs,n_fft,hop", [(120, 2048, 512), (60, 4096, 2048)])
+@pytest.mark.parametrize("secs,n_fft,hop", [(120, 2048, 512), (300, 2048, 512), (60, 4096, 2048)])
 def test_adaptive_quiet_long_stream(secs, n_fft, hop):
     """Quiet input takes the reference's float64 pipeline (SURVEY F6,
     src/process_tomatis_adaptive.py:201-215): levels, threshold, states and
