@@ -8,7 +8,7 @@ computed by the same instructions in either layout (3 warm-up frames rebuild
 the OLA accumulator exactly), and a chunk's scale is the same float32
 limit / peak, so the two layouts must agree bit for bit -- on streams where
 every chunk is limited, none is, or some are, and on stream batches, mono,
-hop 256 / 1024 and time shards.  One configuration is also checked against the
+hop 256 (hop 1024 stays one round) and time shards.  One configuration is also checked against the
 oracle (reference: src/process_tomatis.py:331-357, the per-chunk limiter).
 """
 import numpy as np
@@ -68,7 +68,10 @@ def test_two_rounds_bit_identical(case):
     n = sr * secs + 77
     ss = _scaled(E, torch, ns, n, ch, sr, gains, seed0=400)
     rounds, y2, pk2, pipe = _both(E, torch, ss, n_fft=n_fft, hop=hop)
-    assert rounds == 2, "an eligible standard-mode plan takes two rounds when asked"
+    # hop <= 512 only: round 2's per-sequence LDS slot of a hop block beside the
+    # single-exchange FFT's exchange rows (tm_kernels.hip build_runs)
+    expect = 2 if hop <= 512 else 1
+    assert rounds == expect, "an eligible standard-mode plan takes two rounds when asked"
     assert torch.equal(pipe.peaks, pk2)
     assert torch.equal(pipe.y, y2), "two-round output differs from one round"
     # the limiter property on every stream: chunks over the limit end at it

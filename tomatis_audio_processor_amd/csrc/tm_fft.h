@@ -298,6 +298,143 @@ __device__ __forceinline__ void fft_inv(cf (&v)[NR], int L, const cf* twN, const
   sdft<NR, 2, 0, NR>(v);
 }
 
+// ---------------------------------------------------------------------------
+// Single-exchange FFT (P = 64, NR = 32: n_fft 2048).  Same four-step split
+// n = n1 + 64 n2, k = k2 + 32 k1 as above; the 64-point DFT over the lane
+// index n1 = m + 32 b is done as one radix-2 stage over lane bit 5 followed by
+// a 32-point register DFT, so a direction needs ONE LDS exchange instead of two:
+//   step 3a (lane bit 5 -> register bit): v_permlane32_swap of register pairs
+//     (2j, 2j+1): lane (m, s) then holds Y[m + 32 b, k2 = 2j + s] in register
+//     2j + b; the DIF butterfly over b gives U_e = W_64^{m e} (Y[m] + (-1)^e Y[m+32])
+//     in register 2j + e (one per-lane twiddle W_64^m, on the e = 1 registers);
+//   exchange (one float component at a time, 8.5 KB per wave): every register r
+//     is written as one LDS row by ds_write_addtid_b32 (lane-contiguous, no
+//     address VGPR: the fastest LDS store form, MI355X_MICROARCH.md "LDS"), and
+//     lane (r', s') reads row r' columns 32 s' .. 32 s' + 31 with eight
+//     conflict-free ds_read_b128 (row pitch 68 floats);
+//   step 3b: DFT_32 over m in registers.
+// After the forward transform lane L (r = L & 31, s = L >> 5) register i holds
+// bin k = (2 (r >> 1) + s) + 32 (r & 1) + 64 i with scale splan<32, 0>().sig[i].
+// The inverse walks back; its first DFT's output scales splan<32, 1>().sig[m]
+// stay on lane m (= L & 31) through the exchange and the butterflies and are
+// absorbed by the synthesis window (host table winS).
+// ---------------------------------------------------------------------------
+constexpr int kXPitch = 68;           // floats per exchange row (bank rotation 4)
+constexpr int kXBuf = 32 * kXPitch;   // floats per sequence
+
+__device__ __forceinline__ void swap32(cf& a, cf& b) {  // lanes 32..63 of a <-> lanes 0..31 of b
+  const auto rx = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.x), __float_as_uint(b.x), false, false);
+  const auto ry = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.y), __float_as_uint(b.y), false, false);
+  a = {__uint_as_float(rx[0]), __uint_as_float(ry[0])};
+  b = {__uint_as_float(rx[1]), __uint_as_float(ry[1])};
+}
+
+// eight rows of one component: ds_write_addtid_b32 at M0 + offset + 4 lane.
+// M0 is set inside the block (a SALU write of M0 needs one wait state before
+// an add-TID LDS instruction) and listed as clobbered, so a value the compiler
+// keeps in M0 (LDS-DMA set-up) is re-materialised after it (clang warns that a
+// reserved register is not saved around the statement: nothing needs saving).
+#define TM_ADDTID8(C, R0)                                                           \
+  _Pragma("clang diagnostic push") _Pragma("clang diagnostic ignored \"-Winline-asm\"") \
+  __asm__ volatile(                                                                 \
+      "s_mov_b32 m0, %8\n\ts_nop 0\n\t"                                             \
+      "ds_write_addtid_b32 %0 offset:%9\n\tds_write_addtid_b32 %1 offset:%10\n\t"    \
+      "ds_write_addtid_b32 %2 offset:%11\n\tds_write_addtid_b32 %3 offset:%12\n\t"   \
+      "ds_write_addtid_b32 %4 offset:%13\n\tds_write_addtid_b32 %5 offset:%14\n\t"   \
+      "ds_write_addtid_b32 %6 offset:%15\n\tds_write_addtid_b32 %7 offset:%16"       \
+      ::"v"(v[R0].C), "v"(v[R0 + 1].C), "v"(v[R0 + 2].C), "v"(v[R0 + 3].C),          \
+      "v"(v[R0 + 4].C), "v"(v[R0 + 5].C), "v"(v[R0 + 6].C), "v"(v[R0 + 7].C),        \
+      "s"(base), "n"((R0) * kXPitch * 4), "n"((R0 + 1) * kXPitch * 4),                \
+      "n"((R0 + 2) * kXPitch * 4), "n"((R0 + 3) * kXPitch * 4),                       \
+      "n"((R0 + 4) * kXPitch * 4), "n"((R0 + 5) * kXPitch * 4),                       \
+      "n"((R0 + 6) * kXPitch * 4), "n"((R0 + 7) * kXPitch * 4)                        \
+      : "memory", "m0") _Pragma("clang diagnostic pop")
+
+// transpose (lane, register) through LDS: register r of lane (m, s) -> register
+// m of lane (r, s).  buf: this wave's kXBuf floats (16-B aligned).  LDS
+// operations of one wave complete in order, so each read sees the rows written
+// before it and the second component's writes land after the first's reads;
+// the "memory" clobbers keep the compiler's LDS reads after the writes.
+__device__ __forceinline__ void xchg32(cf (&v)[32], float* buf, int L) {
+  const uint32_t base = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)buf);
+  const float4* rp = reinterpret_cast<const float4*>(buf + (L & 31) * kXPitch + 32 * (L >> 5));
+  TM_ADDTID8(x, 0);
+  TM_ADDTID8(x, 8);
+  TM_ADDTID8(x, 16);
+  TM_ADDTID8(x, 24);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float4 t = rp[q];
+    v[4 * q].x = t.x;
+    v[4 * q + 1].x = t.y;
+    v[4 * q + 2].x = t.z;
+    v[4 * q + 3].x = t.w;
+  }
+  TM_ADDTID8(y, 0);
+  TM_ADDTID8(y, 8);
+  TM_ADDTID8(y, 16);
+  TM_ADDTID8(y, 24);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float4 t = rp[q];
+    v[4 * q].y = t.x;
+    v[4 * q + 1].y = t.y;
+    v[4 * q + 2].y = t.z;
+    v[4 * q + 3].y = t.w;
+  }
+}
+#undef TM_ADDTID8
+
+// forward: v[n2] = x[L + 64 n2] -> bin layout above.  twN: the step-2 table
+// (lane-pair layout, as fft_fwd); w: W_64^{L & 31}.
+__device__ __forceinline__ void fftx_fwd(cf (&v)[32], int L, const cf* twN, cf w, float* buf) {
+  constexpr int P = 64, NR = 32;
+  sdft<NR, 0, 0, NR>(v);
+  sfor<0, NR / 2>([&](auto kk) {
+    constexpr int K2 = decltype(kk)::value;
+    const float4 t = reinterpret_cast<const float4*>(twN)[K2 * P + L];
+    if constexpr (K2 > 0) v[2 * K2] = cmul(v[2 * K2], cf{t.x, t.y});
+    v[2 * K2 + 1] = cmul(v[2 * K2 + 1], cf{t.z, t.w});
+  });
+  sfor<0, NR / 2>([&](auto jj) {
+    constexpr int J = decltype(jj)::value;
+    swap32(v[2 * J], v[2 * J + 1]);
+    const cf a = v[2 * J], b = v[2 * J + 1];
+    v[2 * J] = a + b;
+    v[2 * J + 1] = cmul(a - b, w);
+  });
+  xchg32(v, buf, L);
+  sdft<NR, 0, 0, NR>(v);
+}
+
+// inverse (unnormalised): bin layout -> v[n2] = N x[L + 64 n2] / (sig1[L & 31] sig2[n2])
+__device__ __forceinline__ void fftx_inv(cf (&v)[32], int L, const cf* twN, cf w, float* buf) {
+  constexpr int P = 64, NR = 32;
+  sdft<NR, 1, 0, NR>(v);
+  xchg32(v, buf, L);
+  sfor<0, NR / 2>([&](auto jj) {
+    constexpr int J = decltype(jj)::value;
+    const cf z0 = v[2 * J], z1 = cmulc(v[2 * J + 1], w);
+    v[2 * J] = z0 + z1;
+    v[2 * J + 1] = z0 - z1;
+    swap32(v[2 * J], v[2 * J + 1]);
+  });
+  sfor<0, NR / 2>([&](auto kk) {
+    constexpr int K2 = decltype(kk)::value;
+    const float4 t = reinterpret_cast<const float4*>(twN)[K2 * P + L];
+    if constexpr (K2 > 0) v[2 * K2] = cmulc(v[2 * K2], cf{t.x, t.y});
+    v[2 * K2 + 1] = cmulc(v[2 * K2 + 1], cf{t.z, t.w});
+  });
+  sdft<NR, 2, 0, NR>(v);
+}
+
+// bin index held by lane L, register i after fftx_fwd
+__device__ __forceinline__ int fftx_bin(int L, int i) {
+  const int r = L & 31, s = L >> 5;
+  return (2 * (r >> 1) + s) + 32 * (r & 1) + 64 * i;
+}
+
 // per-lane register tables (window, gains, 1/wsum) in lane-quad layout:
 // element (register i, lane L) at ((i/4)*P + L)*4 + i%4, read with ds_read_b128
 template <int P>

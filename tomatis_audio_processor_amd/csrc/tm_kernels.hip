@@ -1583,6 +1583,7 @@ struct tomatis_plan_s {
   int32_t total_chunks = 0;
   int P = 0, NR = 32, SH = 0, rmax = 1;
   bool generic = false;
+  bool fx = false;  // fused kernel runs the single-exchange FFT (tm_fft.h fftx_*)
   bool lds = false;        // any-size path (k_stft_lds + k_ola_gather_lds)
   float2* twL = nullptr;   // lds path: exp(-2 pi i t / N)
   std::vector<TomatisStream> hs;
@@ -1777,7 +1778,7 @@ static int build_runs(tomatis_plan_s* p) {
   // (auto = one round: measured on C2, round 2's in-loop rescale hides 0.15 ms
   // of tail but the split costs about as much -- DESIGN.md §6)
   const bool two = !p->generic && P == 64 && d.alpha_mode == 0 && p->total_chunks > 0 &&
-                   p->lim_rounds == 2 && N <= 2048;
+                   p->lim_rounds == 2 && N <= 2048 && p->SH <= 8;  // (LDS slots: hop <= 512)
   const int64_t tf_total = std::max<int64_t>(1, p->total_frames);
   // Runs.  Per stream, the emitted frames [e_lo, e_hi) whose run can take the
   // fused kernel's interior loop (full frame loads back to the warm-up frames,
@@ -2092,7 +2093,10 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
                                                              (float)(sin(ang) * sigF[k2])};
         }
       std::vector<float> winS(N);
-      for (int t = 0; t < N; ++t) winS[t] = (float)((double)w[t] * sigI[t / P]);
+      // single-exchange FFT (tm_fft.h fftx_inv): lane m's first-DFT output scale too
+      const bool fx = p->fx;
+      for (int t = 0; t < N; ++t)
+        winS[t] = (float)((double)w[t] * sigI[t / P] * (fx ? splan<32, 1>().sig[(t % P) & 31] : 1.0));
       for (int m = 0; m < P; ++m) {
         const double ang = -2.0 * M_PI * (double)m / (double)P;
         twP[m] = {(float)cos(ang), (float)sin(ang)};
@@ -2271,6 +2275,8 @@ int tomatis_plan_create(tomatis_plan_t* out, const TomatisPlanDesc* desc, const 
     if (s.n_chunks > 1 && (((s.chunk_first - s.first_start) % hop) != 0 || (s.chunk_len % hop) != 0))
       p->generic = true;  // chunk boundaries not on emit blocks: per-sample gather path
   }
+  // n_fft 2048 fused kernels: the single-exchange FFT (its bin layout and scales)
+  p->fx = kFftX && !p->generic && p->P == 64 && p->NR == 32;
   int64_t fb = 0;
   int32_t cb = 0;
   for (int i = 0; i < n_streams; ++i) {
@@ -2653,7 +2659,7 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
       return TOMATIS_E_NOMEM;
     p->gperm_rows = n_rows;
   }
-  launch_gain_perm(p->P, p->NR, gains, n_rows, N / 2 + 1, p->gperm, s);
+  launch_gain_perm(p->P, p->NR, p->fx, gains, n_rows, N / 2 + 1, p->gperm, s);
   MainArgs A;
   A.x = x;
   A.y = y;

@@ -119,13 +119,22 @@ struct LdsArgs {
 void launch_lds_frames(const LdsArgs& A, hipStream_t s);
 void launch_lds_gather(const LdsArgs& A, hipStream_t s);
 
+// n_fft 2048 register kernels (P = 64) run the single-exchange FFT (tm_fft.h
+// fftx_*; its bin layout in the gain rows, its output scales in winS); the
+// two-exchange form stays for n_fft 4096 and for -DTM_DEV_NOFX A/B builds
+#ifdef TM_DEV_NOFX
+constexpr bool kFftX = false;
+#else
+constexpr bool kFftX = true;
+#endif
+
 // launchers (tm_transform.hip); kernels stay private to that unit
 int transform_wg(int P, int NR);  // workgroup size of the fused kernel
 int transform_slots_per_cu(int P, int NR);  // resident sequences per CU
 void launch_transform(const MainArgs& A, int P, int NR, int SH, int ch, int wg, hipStream_t s);
 void launch_frames(const MainArgs& A, int P, int NR, int blocks, hipStream_t s);
-void launch_gain_perm(int P, int NR, const float* gains, int n_rows, int n_bins, float* out,
-                      hipStream_t s);
+void launch_gain_perm(int P, int NR, bool fx, const float* gains, int n_rows, int n_bins,
+                      float* out, hipStream_t s);
 void launch_ola_gather(const MainArgs& A, int n_streams, const int64_t* pos_base, int64_t total,
                        int N, hipStream_t s);
 int dev_opt(int key, int dflt);  // tomatis_set_dev_option (default when unset)

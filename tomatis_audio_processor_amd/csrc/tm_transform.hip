@@ -359,13 +359,14 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   constexpr int HOP = SH * P;
   constexpr int NC = NR - SH;  // carried accumulator registers
   constexpr int SHQ = (SH + 3) & ~3;  // winv registers padded to a quad
-  constexpr bool LT = P == 64;  // per-lane step-3 twiddle table
+  constexpr bool FX = kFftX && P == 64 && NR == 32;  // single-exchange FFT (tm_fft.h fftx_*)
+  constexpr bool LT = P == 64 && !FX;  // per-lane step-3 twiddle table
   __shared__ __attribute__((aligned(16))) cf s_twN[NR * P];
   __shared__ __attribute__((aligned(16))) cf s_twP[LT ? 8 * P : P];
   __shared__ __attribute__((aligned(16))) float s_win[N];      // lane-quad layout
   __shared__ __attribute__((aligned(16))) float s_winS[N];     // synthesis, scaled
   __shared__ __attribute__((aligned(16))) float s_winv[SHQ * P];  // lane-quad layout
-  __shared__ cf s_buf[NSEQ][G::SEQ_LDS];
+  __shared__ __attribute__((aligned(16))) cf s_buf[NSEQ][FX ? kXBuf / 2 : G::SEQ_LDS];
   __shared__ __attribute__((aligned(16))) float s_gain[GM ? 2 * N : 4];
   // PR: one hop block per sequence for the partner rescale (LDS-DMA target)
   __shared__ __attribute__((aligned(16))) char s_pbuf[PR ? NSEQ * SH * P * CH * 4 : 16];
@@ -508,7 +509,8 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
         v[4 * n4 + 3] = cscale(v[4 * n4 + 3], w.w);
       }
       TPROF(1, v[NR - 1].x);
-      fft_fwd<P, NR, LT>(v, L, s_twN, s_twP, buf, A.err);
+      if constexpr (FX) fftx_fwd(v, L, s_twN, s_twP[L & 31], reinterpret_cast<float*>(buf));
+      else fft_fwd<P, NR, LT>(v, L, s_twN, s_twP, buf, A.err);
       TPROF(2, v[NR - 1].x);
       // ---- gain row (real, even, 1/N folded in), per-lane layout ----
       bool g_lds = GM == 1;
@@ -536,7 +538,8 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
         }
       }
       TPROF(3, v[NR - 1].x);
-      fft_inv<P, NR, LT>(v, L, s_twN, s_twP, buf, A.err);
+      if constexpr (FX) fftx_inv(v, L, s_twN, s_twP[L & 31], reinterpret_cast<float*>(buf));
+      else fft_inv<P, NR, LT>(v, L, s_twN, s_twP, buf, A.err);
       TPROF(4, v[NR - 1].x);
       // ---- synthesis window (x the inverse FFT's output scales) + register OLA ----
   #pragma unroll
@@ -1229,7 +1232,8 @@ __global__ __launch_bounds__(256, 2) void k_stft_frames(MainArgs A) {
 
 // gain rows [rows][n_bins] -> [rows][N] in the per-lane bin layout of fft_fwd,
 // mirrored (real even gain) and scaled by 1/N (exact: power of two)
-template <int P, int NR>
+// (FX: the single-exchange FFT's layout, fftx_bin)
+template <int P, int NR, bool FX = false>
 __global__ void k_gain_perm(const float* __restrict__ g, int n_rows, int n_bins,
                             float* __restrict__ out) {
   constexpr int N = NR * P;
@@ -1237,10 +1241,10 @@ __global__ void k_gain_perm(const float* __restrict__ g, int n_rows, int n_bins,
   if (t >= n_rows * N) return;
   const int row = t / N, e = t - row * N;  // e = lq(i, L)
   const int q = e >> 2, L = q % P, i = (q / P) * 4 + (e & 3);
-  int b = fft_bin<P, NR>(L, i);
+  int b = FX ? fftx_bin(L, i) : fft_bin<P, NR>(L, i);
   b = (b <= N / 2) ? b : N - b;
-  // x the forward FFT's output scale of register i (its step-3c DFT_8 output)
-  out[t] = (g[(int64_t)row * n_bins + b] * (1.0f / (float)N)) * sig_at<8>(i & 7);
+  // x the forward FFT's output scale of register i (its last DFT's output)
+  out[t] = (g[(int64_t)row * n_bins + b] * (1.0f / (float)N)) * (FX ? sig_at<32>(i) : sig_at<8>(i & 7));
 }
 
 // generic-hop OLA gather: one thread per output position (frame order preserved)
@@ -1501,7 +1505,7 @@ void launch_main_pf(const MainArgs& A, int ch, hipStream_t s) {
   if constexpr (P == 64 && (SH == 4 || SH == 8)) {
     if (A.gated) {  // in-kernel levels + gate (two-row tables: gm == 1, host-checked)
       if (A.partner) {
-        if constexpr (WG == 512) {
+        if constexpr (WG == 512 && SH <= 8) {
           if (ch == 2)
             hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 1, PF, NT, WG, true, true>), g, b, 0, s, A);
           else
@@ -1515,7 +1519,7 @@ void launch_main_pf(const MainArgs& A, int ch, hipStream_t s) {
       return;
     }
   }
-  if constexpr (P == 64 && WG == 512) {
+  if constexpr (P == 64 && WG == 512 && SH <= 8) {  // (LDS slots: host limits rounds to hop <= 512)
     if (A.partner) {  // round 2 of the two-round limiter (two-row tables: gm == 1)
       if (ch == 2) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 1, PF, NT, WG, true>), g, b, 0, s, A);
       else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, 1, PF, NT, WG, true>), g, b, 0, s, A);
@@ -1557,10 +1561,17 @@ void launch_main(const MainArgs& A, int ch, int wg, hipStream_t s) {
   return launch_main_pf<P, NR, SH, false, true, TM_DEV_WG>(A, ch, s);
 #endif
   if constexpr (P == 64) {
-    // round 2 of the two-round limiter: 512-thread blocks (the per-sequence LDS
+    // single-exchange FFT: 8.5 KB of exchange rows per sequence, so the tables
+    // are shared by 8 sequences (one 512-thread block per CU).  Otherwise round
+    // 2 of the two-round limiter takes 512-thread blocks (the per-sequence LDS
     // slots of the partner rescale fit once per CU)
-    if (wg == 512 || A.partner) return launch_main_pf<P, NR, SH, false, true, 512>(A, ch, s);
-    return launch_main_pf<P, NR, SH, false, true, 256>(A, ch, s);
+    if constexpr (kFftX) {
+      (void)wg;
+      return launch_main_pf<P, NR, SH, false, true, 512>(A, ch, s);
+    } else {
+      if (wg == 512 || A.partner) return launch_main_pf<P, NR, SH, false, true, 512>(A, ch, s);
+      return launch_main_pf<P, NR, SH, false, true, 256>(A, ch, s);
+    }
   }
   if constexpr (P == 128 && NR == 32) {
     if (wg == 512) return launch_main_pf<P, NR, SH, PF, true, 512>(A, ch, s);
@@ -1585,8 +1596,9 @@ int transform_wg(int P, int NR) {
   // two 4-sequence blocks per CU (TOMATIS_WG=512: one 8-sequence block, the
   // same occupancy with one copy of the tables; measured equal).
   // P = 128, NR = 32 (n_fft 4096): 4 two-wave sequences (~120 KB, 2 waves/SIMD).
-  const int dflt = P == 64 ? 256 : (NR == 32 ? 512 : 256);
+  const int dflt = P == 64 ? (kFftX ? 512 : 256) : (NR == 32 ? 512 : 256);
   const int w = dev_opt(TOMATIS_DEV_WG, dflt);
+  if (P == 64 && kFftX) return 512;  // the single-exchange FFT's LDS (see launch_main)
   if (P == 64 && (w == 256 || w == 512)) return w;
   if (P == 128 && NR == 32 && (w == 256 || w == 512)) return w;
   if (P == 128 && NR == 16 && (w == 256 || w == 512 || w == 768)) return w;
@@ -1629,11 +1641,13 @@ void launch_frames(const MainArgs& A, int P, int NR, int blocks, hipStream_t s) 
 #endif
 }
 
-void launch_gain_perm(int P, int NR, const float* gains, int n_rows, int n_bins, float* out,
-                      hipStream_t s) {
+void launch_gain_perm(int P, int NR, bool fx, const float* gains, int n_rows, int n_bins,
+                      float* out, hipStream_t s) {
   const int N = P * NR;
   const int nb = (n_rows * N + 255) / 256;
-  if (P == 64)
+  if (P == 64 && fx)
+    hipLaunchKernelGGL((k_gain_perm<64, 32, true>), dim3(nb), dim3(256), 0, s, gains, n_rows, n_bins, out);
+  else if (P == 64)
     hipLaunchKernelGGL((k_gain_perm<64, 32>), dim3(nb), dim3(256), 0, s, gains, n_rows, n_bins, out);
   else if (NR == 16)
     hipLaunchKernelGGL((k_gain_perm<128, 16>), dim3(nb), dim3(256), 0, s, gains, n_rows, n_bins, out);

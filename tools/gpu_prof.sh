@@ -1,7 +1,7 @@
 #!/bin/bash
-# round 4: kernel stats (C2, C5x) and PMC passes (C2 loud / quiet, C5x)
+# kernel stats (C2, C5x) and PMC passes (C2 loud / quiet, C5x)
 set -o pipefail
-TAG=${1:-r4e}
+TAG=${1:-prof}
 D=gpurun_out/$TAG; mkdir -p $D
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/prof -o c2 -- python3 bench.py --steps 10 --warmup 3 --cpu-sample-s 0 > $D/prof.log 2>&1 || { tail -20 $D/prof.log; exit 1; }

@@ -1,7 +1,7 @@
 #!/bin/bash
-# round 4: full GPU suite, smoke, default bench and the other workloads
+# full GPU suite, smoke, default bench and the other workloads
 set -o pipefail
-TAG=${1:-r4d}
+TAG=${1:-suite}
 D=gpurun_out/$TAG; mkdir -p $D
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $D/gpu_tests.log 2>&1 || { tail -40 $D/gpu_tests.log; exit 1; }
 tail -1 $D/gpu_tests.log
