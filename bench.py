@@ -228,6 +228,9 @@ def main():
                          "PMC traffic runs)")
     ap.add_argument("--cpu-pool-s", type=int, default=300,
                     help="seconds of audio per worker for the all-cores CPU baseline")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="standard mode: every pass applies its own limiter (no batch "
+                         "pipeline: tomatis_stft_ola_gated instead of _pipelined)")
     ap.add_argument("--dev", action="append", default=[], metavar="NAME=VALUE",
                     help="development override (TOMATIS_DEV_<NAME>, A/B experiments); "
                          "recorded in the JSON line's config")
@@ -264,7 +267,10 @@ def main():
             ss.x = engine.scale_copy(ss.x, a.input_gain)
     stages = 1
     if mode == "standard":
-        pipe = engine.GatePipeline(ss, gate_ui=50, n_fft=n_fft, hop=hop)
+        # batch pipeline: pass k+1's transform applies pass k's limiter in its
+        # frame loops; the timed region ends with flush() (the last pass's limiter)
+        pipe = engine.GatePipeline(ss, gate_ui=50, n_fft=n_fft, hop=hop,
+                                   pipelined=not a.no_pipeline)
     elif mode == "xfade":
         pipe = engine.GatePipeline(ss, gate_ui=50, gate_offset=-90, n_fft=n_fft, hop=hop,
                                    xfade_ms=500.0)
@@ -288,6 +294,8 @@ def main():
     t0 = time.perf_counter()
     for k in range(a.steps):
         pipe.run(marks=marks[k], check_device=False)
+    if hasattr(pipe, "flush"):
+        pipe.flush()        # pipelined: the last pass's limiter, inside the timed region
     torch.cuda.synchronize()
     if ws > 1:
         dist.barrier()
@@ -349,6 +357,7 @@ def main():
                                        f"all_reduce)" if strong else
                                        f"file-parallel x{ws} (RCCL manifest all_gather)"),
                        "fused_levels": bool(getattr(pipe, "gated_used", False)),
+                       "pipelined": bool(getattr(pipe, "pipelined", False)),
                        **({"dev_overrides": a.dev} if a.dev else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -62,7 +62,7 @@
 extern "C" {
 #endif
 
-#define TOMATIS_ABI_VERSION 6
+#define TOMATIS_ABI_VERSION 7
 
 #define TOMATIS_OK 0
 #define TOMATIS_E_ARG (-1)        /* bad argument */
@@ -268,6 +268,23 @@ int tomatis_stft_ola_gated_after_lookback(tomatis_plan_t plan, const float* x,
                                           const float* gain_rows, int32_t n_rows, float* y,
                                           uint32_t* chunk_peak_bits, float limit, float* r_out,
                                           uint8_t* states_out, void* hip_stream);
+/* Pipelined batches of one plan (batch k+1's transform limits batch k's
+ * output): as tomatis_stft_ola_gated_after_lookback with limit > 0, except that
+ * y is left UNSCALED (chunk_peak_bits complete when the launch does) and, when
+ * prev_y is given, the previous batch's unscaled output prev_y (written by the
+ * previous call with this plan, its peaks prev_peak_bits) gets the per-chunk
+ * limiter of src/process_tomatis.py:331-357 inside this launch's frame loops --
+ * so the rescale's HBM traffic overlaps the transform instead of being a tail.
+ * The last batch's output is limited by tomatis_apply_limiter(plan, y,
+ * chunk_peak_bits, limit).  Results are bit-identical to the unpipelined call.
+ * y, chunk_peak_bits must not alias prev_y, prev_peak_bits.
+ * TOMATIS_E_UNSUPPORTED where tomatis_stft_ola_gated is, or without limiter
+ * chunks (the caller runs the unpipelined call). */
+int tomatis_stft_ola_gated_pipelined(tomatis_plan_t plan, const float* x,
+                                     const float* gain_rows, int32_t n_rows, float* y,
+                                     uint32_t* chunk_peak_bits, float limit, float* r_out,
+                                     uint8_t* states_out, float* prev_y,
+                                     const uint32_t* prev_peak_bits, void* hip_stream);
 /* The limiter on the edge chunks of edge_mask only. */
 int tomatis_apply_limiter_edges(tomatis_plan_t plan, float* y, const uint32_t* chunk_peak_bits,
                                 float limit, int32_t edge_mask, void* hip_stream);
@@ -345,6 +362,8 @@ int32_t tomatis_plan_limiter_rounds(tomatis_plan_t plan);
 #define TOMATIS_DEV_LIMITER_ROUNDS 13  /* initial TOMATIS_OPT_LIMITER_ROUNDS of new plans */
 #define TOMATIS_DEV_FUSED_LEVELS 14    /* 0: tomatis_stft_ola_gated declines (host two-pass) */
 int tomatis_set_dev_option(int32_t key, int32_t value);
+/* The current override of key (-1: default, or an unknown key). */
+int32_t tomatis_get_dev_option(int32_t key);
 
 /* FLAC frames encoded on the device (row f1 egress; src/process_tomatis.py:
  * 242-251,357 write the output through libsndfile's FLAC PCM_24 encoder).

@@ -1,0 +1,160 @@
+"""GPU: pipelined batches (tomatis_stft_ola_gated_pipelined, DESIGN.md §6
+"Pipelined limiter") against unpipelined passes.
+
+Each pipelined pass leaves its own output unscaled and applies the per-chunk
+limiter of the previous pass's output inside its frame loops (the same
+float32 ``limit / peak`` multiply the fused limiter applies,
+src/process_tomatis.py:331-357); flush() limits the last one.  Every pass's
+final output, chunk peaks, r and states must equal an unpipelined pass over
+the same input bit for bit -- with a different input each pass, limited and
+quiet chunks, stream batches, mono / hop 256, ragged streams (edge runs whose
+partner blocks all go to the tail) and a pass whose gate look-back fails (the
+two-pass redo of that pass, the previous pass still limited by its launch).
+"""
+import numpy as np
+import pytest
+
+from tomatis_audio_processor_amd.synth import synth_stream
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from tomatis_audio_processor_amd import engine
+    return torch, engine
+
+
+def _inputs(E, torch, ns, n, ch, sr, gains, passes):
+    """per pass: a device input of the same geometry (seeds and gains vary)"""
+    out = []
+    for k in range(passes):
+        ss = E.StreamSet.synthetic(ns, n, ch, sr, seed0=700 + 31 * k)
+        for i, g in enumerate(gains):
+            gk = g * (1.0, 0.4, 1.3)[k % 3]
+            if gk != 1.0:
+                o = ss.offs[i]
+                ss.x[o:o + n * ch] *= gk
+        out.append(ss.x.clone())
+    return out
+
+
+def _unpipelined(E, ss, xs, **kw):
+    pipe = E.GatePipeline(ss, **kw)
+    refs = []
+    for x in xs:
+        ss.x.copy_(x)
+        pipe.run()
+        assert pipe.gated_used and not pipe.pending
+        refs.append((pipe.y.clone(), pipe.peaks.clone(), pipe.r.clone(), pipe.states.clone()))
+    return refs
+
+
+def _check(torch, F, got, ref, k):
+    y, pk, r, st = got
+    ry, rpk, rr, rst = ref
+    assert torch.equal(st[:F], rst[:F]), f"pass {k}: states differ"
+    assert torch.equal(r[:F].view(torch.int32), rr[:F].view(torch.int32)), f"pass {k}: r differs"
+    assert torch.equal(pk, rpk), f"pass {k}: chunk peaks differ"
+    assert torch.equal(y, ry), f"pass {k}: output differs"
+
+
+def _pipelined(torch, E, ss, xs, refs, **kw):
+    pipe = E.GatePipeline(ss, pipelined=True, **kw)
+    F = pipe.plan.total_frames
+    held = None
+    for k, x in enumerate(xs):
+        ss.x.copy_(x)
+        assert pipe.run() is None, "a pipelined pass returns no (unlimited) result"
+        assert pipe.pipelined and pipe.pending and pipe.gated_used
+        if held is not None:  # the previous pass's buffer is final now
+            _check(torch, F, (held[0].clone(), held[1].clone(), held[2], held[3]), refs[k - 1], k - 1)
+        # r / states are per pass (the next pass overwrites them)
+        held = (pipe.y, pipe.peaks, pipe.r.clone(), pipe.states.clone())
+    res = pipe.result()  # flushes the last pass
+    assert not pipe.pending
+    _check(torch, F, (res.y, res.chunk_peaks, held[2], held[3]), refs[-1], len(xs) - 1)
+    return pipe
+
+
+@pytest.mark.parametrize("case", [
+    # (streams, seconds, ch, sr, hop, per-stream input gains)
+    ("c2_like", 1, 600, 2, 44100, 512, [1.0]),
+    ("batch_mixed", 6, 60, 2, 48000, 512, [1.0, 0.05, 0.3, 1.0, 0.15, 0.6]),
+    ("mono_hop256", 3, 40, 1, 44100, 256, [1.0, 0.2, 0.02]),
+    ("short", 4, 2, 2, 44100, 512, [1.0, 0.5, 0.1, 1.0]),
+])
+def test_pipelined_bit_identical(case):
+    torch, E = _engine()
+    _, ns, secs, ch, sr, hop, gains = case
+    n = sr * secs + 391
+    xs = _inputs(E, torch, ns, n, ch, sr, gains, 3)
+    ss = E.StreamSet.synthetic(ns, n, ch, sr, seed0=1)
+    kw = dict(gate_ui=50, n_fft=2048, hop=hop)
+    refs = _unpipelined(E, ss, xs, **kw)
+    _pipelined(torch, E, ss, xs, refs, **kw)
+
+
+def test_pipelined_ragged():
+    """Edge runs (stream heads / tails, streams shorter than an interior run):
+    their partner blocks are limited in the runs' tails."""
+    torch, E = _engine()
+    sr = 44100
+    lens = [sr * 70 + 13, 1500, sr * 3 + 1, 2048, sr * 41 + 999]
+    xs_np = [[synth_stream(31 + i + 7 * k, n, 2, sr) * (1.0, 0.5)[k % 2] for i, n in enumerate(lens)]
+             for k in range(3)]
+    ss = E.StreamSet.from_arrays(xs_np[0], sr)
+    xs = [E.StreamSet.from_arrays(a, sr).x.clone() for a in xs_np]
+    kw = dict(gate_ui=50, n_fft=2048, hop=512)
+    refs = _unpipelined(E, ss, xs, **kw)
+    _pipelined(torch, E, ss, xs, refs, **kw)
+
+
+def test_pipelined_gate_fallback():
+    """Pass 1's input hovers at the gate threshold (look-back unresolved): that
+    pass is redone on the two-pass chain, limited; pass 0 was limited by pass
+    1's launch all the same, and pass 2 pipelines again from pass 1."""
+    torch, E = _engine()
+    sr, hop = 44100, 512
+    n = hop * 1400
+    amp = np.sqrt(2.0) * 10.0 ** (-40.0 / 20.0)
+    s = (amp * np.sin(2 * np.pi * 1000.0 * np.arange(n) / sr)).astype(np.float32)
+    hover = np.stack([s, s], 1)
+    loud = [synth_stream(8 + k, n, 2, sr) for k in range(3)]
+    arrays = [[loud[0], loud[1]], [hover, loud[1]], [loud[2], loud[0]]]
+    ss = E.StreamSet.from_arrays(arrays[0], sr)
+    xs = [E.StreamSet.from_arrays(a, sr).x.clone() for a in arrays]
+    kw = dict(gate_ui=50, n_fft=2048, hop=hop)
+    two = E.GatePipeline(ss, fused_levels=False, **kw)
+    refs = []
+    for x in xs:
+        ss.x.copy_(x)
+        two.run()
+        refs.append((two.y.clone(), two.peaks.clone(), two.r.clone(), two.states.clone()))
+    pipe = E.GatePipeline(ss, pipelined=True, **kw)
+    F = pipe.plan.total_frames
+    ss.x.copy_(xs[0])
+    pipe.run()
+    y0, pk0 = pipe.y, pipe.peaks
+    ss.x.copy_(xs[1])
+    res1 = pipe.run()  # flagged and redone: limited at once
+    assert pipe.gate_fallbacks == 1 and not pipe.pending and res1 is not None
+    _check(torch, F, (y0, pk0, refs[0][2], refs[0][3]), refs[0], 0)
+    _check(torch, F, (pipe.y, pipe.peaks, pipe.r, pipe.states), refs[1], 1)
+    ss.x.copy_(xs[2])
+    assert pipe.run() is None and pipe.pending
+    res = pipe.result()
+    _check(torch, F, (res.y, res.chunk_peaks, pipe.r, pipe.states), refs[2], 2)
+
+
+def test_pipelined_declines():
+    """hop 1024 (no fused gate) and xfade run unpipelined, results at once."""
+    torch, E = _engine()
+    sr, n = 44100, 44100 * 20
+    ss = E.StreamSet.synthetic(1, n, 2, sr, seed0=5)
+    for kw in (dict(n_fft=2048, hop=1024), dict(n_fft=2048, hop=512, xfade_ms=500.0)):
+        pipe = E.GatePipeline(ss, gate_ui=50, pipelined=True, **kw)
+        res = pipe.run()
+        assert res is not None and not pipe.pending, kw

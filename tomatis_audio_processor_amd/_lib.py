@@ -14,7 +14,7 @@ import ctypes as C
 import os
 
 LIB_NAME = "libtomatis_hip.so"
-ABI_VERSION = 6  # include/tomatis_hip.h TOMATIS_ABI_VERSION
+ABI_VERSION = 7  # include/tomatis_hip.h TOMATIS_ABI_VERSION
 GATE_SEGMENT = 1024      # TOMATIS_GATE_SEGMENT
 GATE_NONE = -536870912   # TOMATIS_GATE_NONE
 ERR_LIMITER_WAIT = 1     # TOMATIS_ERR_LIMITER_WAIT
@@ -112,6 +112,8 @@ _SIGS = {
                                        C.c_int64, _P, C.c_int64, _P, _P]),
     "tomatis_stft_ola_gated_after_lookback": (C.c_int, [_P, _P, _P, C.c_int32, _P, _P, C.c_float,
                                                         _P, _P, _P]),
+    "tomatis_stft_ola_gated_pipelined": (C.c_int, [_P, _P, _P, C.c_int32, _P, _P, C.c_float,
+                                                   _P, _P, _P, _P, _P]),
     "tomatis_ts_summary": (C.c_int, [_P, _P, C.c_int32, C.c_int32, _P, _P]),
     "tomatis_ts_gate": (C.c_int, [_P, _P, _P, C.c_int32, C.c_int32, _P, _P, _P]),
     "tomatis_plan_error": (C.c_int, [_P, _P]),
@@ -119,6 +121,7 @@ _SIGS = {
     "tomatis_plan_set_option": (C.c_int, [_P, C.c_int32, C.c_int64]),
     "tomatis_plan_limiter_rounds": (C.c_int32, [_P]),
     "tomatis_set_dev_option": (C.c_int, [C.c_int32, C.c_int32]),
+    "tomatis_get_dev_option": (C.c_int32, [C.c_int32]),
     "tomatis_absmax": (C.c_int, [_P, C.c_int64, _P, _P]),
     "tomatis_absmax_streams": (C.c_int, [_P, _P, _P, _P]),
     "tomatis_scale_copy": (C.c_int, [_P, _P, C.c_int64, C.c_float, _P]),
@@ -202,19 +205,28 @@ def set_dev_option(name: str, value: int):
     check(lib().tomatis_set_dev_option(DEV_KEYS[name], int(value)), "set_dev_option")
 
 
+def get_dev_option(name: str) -> int:
+    """The current override of TOMATIS_DEV_<name> (-1: the default)."""
+    return int(lib().tomatis_get_dev_option(DEV_KEYS[name]))
+
+
 class dev_options:
     """Context manager: ``with dev_options(RUN_FRAMES=48, FAST_LOOP=0): ...``
-    sets development overrides and restores the defaults on exit."""
+    sets development overrides and restores the values they had on entry
+    (nested contexts and earlier set_dev_option calls survive).  The overrides
+    are process-wide: set them while no other thread creates plans."""
 
     def __init__(self, **kw):
         self.kw = kw
+        self.saved = {}
 
     def __enter__(self):
+        self.saved = {k: get_dev_option(k) for k in self.kw}
         for k, v in self.kw.items():
             set_dev_option(k, v)
         return self
 
     def __exit__(self, *exc):
-        for k in self.kw:
-            set_dev_option(k, -1)
+        for k, v in self.saved.items():
+            set_dev_option(k, v)
         return False

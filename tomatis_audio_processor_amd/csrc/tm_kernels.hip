@@ -1647,6 +1647,10 @@ struct tomatis_plan_s {
   uint32_t* chunk_final = nullptr;
   uint32_t* pieces = nullptr;
   int max_pieces = 0;
+  // pipelined batches (tomatis_stft_ola_gated_pipelined): per run the previous
+  // batch's blocks to rescale in the frame loop (k_r2_plan output)
+  uint32_t* xs_pieces = nullptr;
+  int xs_max_pieces = 0;
   // in-kernel levels + gate (tomatis_stft_ola_gated): per-run carry-in
   int32_t* gate_carry = nullptr;
   float* gate_win = nullptr;
@@ -1737,7 +1741,7 @@ int tomatis_plan_destroy(tomatis_plan_t p) {
                   p->grp_base, p->leaf_base, p->leaves, p->gsum, p->gcarry, p->gcarry_in,
                   p->aq, p->afin, p->acin,
                   p->chunk_need, p->chunk_done, p->chunk_rng, p->err, p->twL,
-                  p->partner, p->chunk_final, p->pieces, p->gate_carry, p->gate_win,
+                  p->partner, p->chunk_final, p->pieces, p->xs_pieces, p->gate_carry, p->gate_win,
                   p->pw_leaf, p->pw_prog, p->blue_b, p->blue_h, p->glb_work};
   for (void* q : ptrs) dfree(q);
   delete p;
@@ -1944,6 +1948,9 @@ static int limiter_accounting(tomatis_plan_s* p) {
   p->chunk_final = nullptr;
   p->pieces = nullptr;
   p->max_pieces = 0;
+  dfree(p->xs_pieces);  // re-sized for these runs on the next pipelined batch
+  p->xs_pieces = nullptr;
+  p->xs_max_pieces = 0;
   if (p->n1 > 0) {
     const int nr = (int)runs.size(), n1 = p->n1, n2 = nr - n1;
     std::vector<int32_t> partner(nr, -1);
@@ -2609,9 +2616,29 @@ static int gate_lookback(tomatis_plan_s* p, const float* x, hipStream_t s) {
   return launch_check();
 }
 
+// the previous batch of a pipelined call (tomatis_stft_ola_gated_pipelined)
+struct PrevBatch {
+  float* y;               // its unscaled output (nullptr: first batch)
+  const uint32_t* peaks;  // its final chunk peaks
+};
+
+// piece lists of the pipelined partner rescale: every run's own emitted blocks
+static int xs_pieces_alloc(tomatis_plan_s* p) {
+  if (p->xs_pieces) return TOMATIS_OK;
+  int mp = 1;
+  for (const Run& R : p->hruns)
+    mp = std::max<int>(mp, (int)(R.kb - std::max<int64_t>(0, R.ka - (p->rmax - 1))));
+  if (hipMalloc(reinterpret_cast<void**>(&p->xs_pieces),
+                (size_t)std::max(1, p->n_runs) * 2 * (mp + 1) * sizeof(uint32_t)))
+    return TOMATIS_E_NOMEM;
+  p->xs_max_pieces = mp;
+  return TOMATIS_OK;
+}
+
 static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, int32_t n_rows,
                          const uint16_t* rows, float* y, uint32_t* peaks, float limit,
-                         void* hs, const GateOut* gate = nullptr) {
+                         void* hs, const GateOut* gate = nullptr,
+                         const PrevBatch* prev = nullptr) {
   if (!p || !x || !gains || (!rows && !gate) || !y || !peaks || n_rows < 1) return TOMATIS_E_ARG;
   if (p->n_runs == 0) return TOMATIS_OK;
   hipStream_t s = (hipStream_t)hs;
@@ -2715,6 +2742,8 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
   A.st_out = nullptr;
   A.gcarry = nullptr;
   A.gwin = nullptr;
+  A.yprev = nullptr;
+  A.peaks_prev = nullptr;
   if (gate) {
     // per run: the carry-in state id and leaf window (k_gate_carry), then the
     // transform computes every frame's r and state from the input it loads
@@ -2740,6 +2769,26 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
     int rc = launch_check();
     if (rc || p->total_out == 0) return rc;
     launch_ola_gather(A, p->n_streams, p->pos_base, p->total_out, N, s);
+    return launch_check();
+  }
+  if (prev) {
+    // pipelined batch: this output stays unscaled for the next batch (its peaks
+    // complete when the launch does); the previous batch's output, complete,
+    // is limited block by block inside this launch's frame loops (k_r2_plan
+    // lists each run's blocks of chunks over the limit), the rest in the runs'
+    // tails -- no wave waits, and the rescale traffic overlaps the transform
+    A.defer_self = 1;
+    if (prev->y) {
+      int rc = xs_pieces_alloc(p);
+      if (rc) return rc;
+      A.yprev = prev->y;
+      A.peaks_prev = prev->peaks;
+      A.pieces = p->xs_pieces;
+      A.max_pieces = p->xs_max_pieces;
+      launch_r2_plan(A, nullptr, p->xs_pieces, s);
+      if ((rc = launch_check())) return rc;
+    }
+    launch_transform(A, p->P, p->NR, p->SH, ch, transform_wg(p->P, p->NR), s);
     return launch_check();
   }
 #ifdef TM_PROFILE
@@ -2882,6 +2931,22 @@ int tomatis_stft_ola_gated_after_lookback(tomatis_plan_t p, const float* x, cons
   return stft_ola_gated(p, x, gains, n_rows, y, peaks, limit, r_out, states_out, true, hs);
 }
 
+int tomatis_stft_ola_gated_pipelined(tomatis_plan_t p, const float* x, const float* gains,
+                                     int32_t n_rows, float* y, uint32_t* peaks, float limit,
+                                     float* r_out, uint8_t* states_out, float* prev_y,
+                                     const uint32_t* prev_peaks, void* hs) {
+  if (!p || !x || !gains || !y || !peaks || !r_out || !states_out || n_rows != 2 ||
+      !(limit > 0.f) || (prev_y && (!prev_peaks || prev_y == y || prev_peaks == peaks)))
+    return TOMATIS_E_ARG;
+  // the kernel's partner-rescale instantiation: interior loop, two LDS gain rows,
+  // hop <= 512 (gated_eligible), per-chunk accounting
+  if (!gated_eligible(p) || p->total_chunks <= 0 || !p->chunk_need || p->SH > 8)
+    return TOMATIS_E_UNSUPPORTED;
+  const GateOut g{r_out, states_out, true};
+  const PrevBatch pb{prev_y, prev_peaks};
+  return stft_ola_impl(p, x, gains, n_rows, nullptr, y, peaks, limit, hs, &g, &pb);
+}
+
 int tomatis_stft_ola_limited(tomatis_plan_t p, const float* x, const float* gains,
                              int32_t n_rows, const uint16_t* rows, float* y, uint32_t* peaks,
                              float limit, void* hs) {
@@ -2934,6 +2999,11 @@ int tomatis_set_dev_option(int32_t key, int32_t value) {
   if (key <= 0 || key >= tshared::kDevKeys) return TOMATIS_E_ARG;
   tshared::g_dev[key] = value < 0 ? -1 : value;
   return TOMATIS_OK;
+}
+
+int32_t tomatis_get_dev_option(int32_t key) {
+  if (key <= 0 || key >= tshared::kDevKeys) return -1;
+  return tshared::g_dev[key];
 }
 
 int32_t tomatis_plan_limiter_rounds(tomatis_plan_t p) {

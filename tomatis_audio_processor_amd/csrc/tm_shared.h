@@ -69,6 +69,12 @@ struct MainArgs {
   // left to the tail}, then count x {partner block, scale bits}
   const uint32_t* pieces;
   int max_pieces;
+  // Pipelined batches (tomatis_stft_ola_gated_pipelined): the partner of every
+  // run is the same run of the PREVIOUS batch of this plan, whose unscaled
+  // output yprev and final chunk peaks peaks_prev are complete (no waits); the
+  // kernel's own output stays unscaled (defer_self) for the next batch.
+  float* yprev;
+  const uint32_t* peaks_prev;
   // in-kernel levels + gate (tomatis_stft_ola_gated, DESIGN.md §5 "Fused
   // levels"): every frame's r (numpy pairwise order) and gate state are computed
   // from the input the transform loads and written here; each run starts from

@@ -85,29 +85,34 @@ __device__ __forceinline__ void flush_peak(float& pk, int cid, const TomatisStre
 // fused limiter tail of one wave: wait until every flush of chunk gc has been
 // counted (all contributors are dispatched no later than this wave's
 // neighbours), then scale this wave's own samples of the chunk.
+// prev: the previous pipelined batch's chunk gc (final: no wait; its peaks and
+// output from A.peaks_prev / A.yprev)
 template <int CH>
 __device__ void limit_own(const MainArgs& A, const TomatisStream& S, int gc, int64_t lo,
-                          int64_t hi, int lane) {
-  const uint32_t need = A.chunk_need[gc];
-  uint32_t got = 0;
-  for (int spin = 0; spin < A.lim_spin; ++spin) {
-    got = __hip_atomic_load(A.chunk_done + gc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    got = __builtin_amdgcn_readfirstlane(got);
-    if (got >= need) break;
-    __builtin_amdgcn_s_sleep(32);
-  }
-  if (got < need) {  // never expected; leaves the chunk unscaled and reports it (the
-    // host re-runs the launch unfused, engine.py _finish)
-    if (lane == 0) atomicOr(A.err, TOMATIS_ERR_LIMITER_WAIT);
-    return;
+                          int64_t hi, int lane, bool prev = false) {
+  if (!prev) {
+    const uint32_t need = A.chunk_need[gc];
+    uint32_t got = 0;
+    for (int spin = 0; spin < A.lim_spin; ++spin) {
+      got = __hip_atomic_load(A.chunk_done + gc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      got = __builtin_amdgcn_readfirstlane(got);
+      if (got >= need) break;
+      __builtin_amdgcn_s_sleep(32);
+    }
+    if (got < need) {  // never expected; leaves the chunk unscaled and reports it (the
+      // host re-runs the launch unfused, engine.py _finish)
+      if (lane == 0) atomicOr(A.err, TOMATIS_ERR_LIMITER_WAIT);
+      return;
+    }
   }
   const float peak = __uint_as_float(__builtin_amdgcn_readfirstlane(
-      __hip_atomic_load(A.peaks + gc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+      __hip_atomic_load((prev ? A.peaks_prev : A.peaks) + gc, __ATOMIC_RELAXED,
+                        __HIP_MEMORY_SCOPE_AGENT)));
   if (!(peak > A.limit)) return;
   const float sc = A.limit / peak;
   const int64_t a = max(lo, A.chunk_rng[2 * gc]), b = min(hi, A.chunk_rng[2 * gc + 1]);
   if (b <= a) return;
-  float* base = A.y + S.out_off + a * CH;
+  float* base = (prev ? A.yprev : A.y) + S.out_off + a * CH;
   int64_t n = (b - a) * CH;
   // scalar head up to 16-byte alignment, float4 body (16 in flight per lane), tail
   const int head = (int)min<int64_t>(n, (4 - (int)((reinterpret_cast<uintptr_t>(base) >> 2) & 3)) & 3);
@@ -649,7 +654,9 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
     int np = 0;
     float* yP = ys;
     if constexpr (PR) {
-      const int pr = __builtin_amdgcn_readfirstlane(A.partner[run_id]);
+      // partner: a round-1 run of this launch, or (pipelined) this run's slot in
+      // the previous batch's output
+      const int pr = A.yprev ? run_id : __builtin_amdgcn_readfirstlane(A.partner[run_id]);
       plist = (cu32*)(A.pieces) + (int64_t)run_loc * 2 * (A.max_pieces + 1);
       np = (int)plist[0];
       if (np > 0) {
@@ -658,7 +665,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
         const int64_t off = SP.out_off + CH * (SP.first_start + RP.ka * HOP - SP.out_begin);
         const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)off);
         const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)off >> 32));
-        yP = A.y + (int64_t)(((uint64_t)hi << 32) | lo);
+        yP = (A.yprev ? A.yprev : A.y) + (int64_t)(((uint64_t)hi << 32) | lo);
       }
     }
     uint32_t rw_nx = GT ? 0u : row_word(0);  // (GT: no row ids)
@@ -882,7 +889,8 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
     }
   }
   if constexpr (PR) {  // the partner's output not scaled in the frame loop
-    const int pr = valid ? A.partner[run_id] : -1;
+    const bool prev = A.yprev != nullptr;  // previous batch: final, no waits
+    const int pr = valid ? (prev ? run_id : A.partner[run_id]) : -1;
     if (pr >= 0 && done) {
       const Run RP = A.runs[pr];
       const TomatisStream SP = A.st[RP.s];
@@ -898,7 +906,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
         const int c0 = chunk_of(lo + SP.out_begin, SP), c1 = chunk_of(hi - 1 + SP.out_begin, SP);
         for (int c = c0; c <= c1; ++c) {
           if (((A.edge_mask & 1) && c == 0) || ((A.edge_mask & 2) && c == SP.n_chunks - 1)) continue;
-          limit_own<CH>(A, SP, SP.chunk_base + c, wlo, whi, L & 63);
+          limit_own<CH>(A, SP, SP.chunk_base + c, wlo, whi, L & 63, prev);
         }
       }
     }
@@ -928,7 +936,8 @@ __global__ __launch_bounds__(64) void k_r2_plan(MainArgs A, const uint32_t* __re
   if (t >= A.n_runs) return;
   uint32_t* o = out + (int64_t)t * 2 * (A.max_pieces + 1);
   const int run = A.run_base + t;
-  const int pr = A.partner[run];
+  const bool prev = A.yprev != nullptr;  // pipelined: the same run of the previous batch
+  const int pr = prev ? run : A.partner[run];
   int n = 0, stop = 0;
   if (pr >= 0 && (A.runs[pr].last & kRunInterior) && (A.runs[run].last & kRunInterior)) {
     const Run R = A.runs[run], RP = A.runs[pr];
@@ -950,10 +959,10 @@ __global__ __launch_bounds__(64) void k_r2_plan(MainArgs A, const uint32_t* __re
       if (j < nb) {
         const int c = chunk_of(s0 + (int64_t)j * hop, SP);
         const int g = SP.chunk_base + c;
-        halt = !chunk_final[g] ||
+        halt = (!prev && !chunk_final[g]) ||
                ((A.edge_mask & 1) && c == 0) || ((A.edge_mask & 2) && c == SP.n_chunks - 1);
         if (!halt) {
-          const float peak = __uint_as_float(A.peaks[g]);
+          const float peak = __uint_as_float((prev ? A.peaks_prev : A.peaks)[g]);
           want = peak > A.limit;
           sc = A.limit / peak;
         }
@@ -1504,7 +1513,7 @@ void launch_main_pf(const MainArgs& A, int ch, hipStream_t s) {
   const dim3 g((A.n_runs + WG / P - 1) / (WG / P)), b(WG);
   if constexpr (P == 64 && (SH == 4 || SH == 8)) {
     if (A.gated) {  // in-kernel levels + gate (two-row tables: gm == 1, host-checked)
-      if (A.partner) {
+      if (A.partner || A.yprev) {
         if constexpr (WG == 512 && SH <= 8) {
           if (ch == 2)
             hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 1, PF, NT, WG, true, true>), g, b, 0, s, A);
@@ -1520,7 +1529,7 @@ void launch_main_pf(const MainArgs& A, int ch, hipStream_t s) {
     }
   }
   if constexpr (P == 64 && WG == 512 && SH <= 8) {  // (LDS slots: host limits rounds to hop <= 512)
-    if (A.partner) {  // round 2 of the two-round limiter (two-row tables: gm == 1)
+    if (A.partner || A.yprev) {  // round 2 / pipelined batch (two-row tables: gm == 1)
       if (ch == 2) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 1, PF, NT, WG, true>), g, b, 0, s, A);
       else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, 1, PF, NT, WG, true>), g, b, 0, s, A);
       return;
@@ -1569,7 +1578,7 @@ void launch_main(const MainArgs& A, int ch, int wg, hipStream_t s) {
       (void)wg;
       return launch_main_pf<P, NR, SH, false, true, 512>(A, ch, s);
     } else {
-      if (wg == 512 || A.partner) return launch_main_pf<P, NR, SH, false, true, 512>(A, ch, s);
+      if (wg == 512 || A.partner || A.yprev) return launch_main_pf<P, NR, SH, false, true, 512>(A, ch, s);
       return launch_main_pf<P, NR, SH, false, true, 256>(A, ch, s);
     }
   }

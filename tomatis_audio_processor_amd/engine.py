@@ -392,13 +392,21 @@ class GatePipeline:
                  dynamic_range=80.0, gate_scale=1.0, gate_offset=-100, hysteresis_db=3.0,
                  fc=1000.0, slope=12.0, c1_low=15.0, c1_high=-15.0, c2_low=-15.0,
                  c2_high=15.0, up_delay_ms=250.0, n_fft=4096, hop=2048,
-                 output_gain_db=0.0, xfade_ms=None, geometry=None, fused_levels=True):
+                 output_gain_db=0.0, xfade_ms=None, geometry=None, fused_levels=True,
+                 pipelined=False):
         """``geometry``: optional per-stream dicts (first_start, n_frames,
         out_begin, out_len, chunk_first, chunk_len, n_chunks) replacing the
         reference schedule -- a time shard of a longer stream (timeshard.py).
         ``fused_levels``: standard mode computes levels and gate states inside
         the transform kernel (tomatis_stft_ola_gated) where the library takes
-        the shape; False, or a shape it declines, runs the two-pass chain."""
+        the shape; False, or a shape it declines, runs the two-pass chain.
+        ``pipelined``: successive run() calls form a batch pipeline
+        (tomatis_stft_ola_gated_pipelined): each pass leaves its output
+        unscaled and limits the PREVIOUS pass's output inside its own transform
+        (two output buffers, alternating), so the limiter's HBM re-read overlaps
+        compute instead of ending every pass.  A pass's output is final after
+        the next run() or flush(); result() flushes.  Same results bit for bit.
+        Shapes the pipelined call declines run unpipelined."""
         torch = _torch()
         _check_fft(n_fft, hop, ss.ch)
         self.ss, self.n_fft, self.hop = ss, n_fft, hop
@@ -477,6 +485,12 @@ class GatePipeline:
         self.fused_levels = bool(fused_levels) and not self.xfade
         self.gated_used = False   # the last run() took tomatis_stft_ola_gated
         self.gate_fallbacks = 0   # gated passes re-run on the two-pass chain
+        self.pipelined = bool(pipelined) and self.fused_levels
+        self.pending = False      # pipelined: self.y awaits its limiter
+        if self.pipelined:
+            self._ys = [self.y, torch.empty_like(self.y)]
+            self._pks = [self.peaks, torch.zeros_like(self.peaks)]
+            self._cur = 0
 
     def run(self, marks=None, check_device: bool = True):
         """Launch the whole chain on the current stream.
@@ -493,7 +507,8 @@ class GatePipeline:
                     marks[1].record()
                 if check_device:
                     self.finish()
-                return self.result()
+                # pipelined: the output is final after the next pass or flush()
+                return None if self.pending else self.result()
             self.fused_levels = False  # declined: this plan's shape runs two passes
         self._two_pass(marks)
         if check_device:
@@ -510,6 +525,9 @@ class GatePipeline:
         if rc == E_UNSUPPORTED:
             return False
         check(rc, "gate_lookback")
+        if self.pipelined and self._pipelined_pass(marks):
+            return True
+        self.flush()
         self.peaks.zero_()
         if marks:
             marks[0].record()
@@ -517,6 +535,38 @@ class GatePipeline:
             self.plan.h, ptr(self.ss.x), ptr(self.gains), self.n_rows, ptr(self.y),
             ptr(self.peaks), PEAK_LIMIT, ptr(self.r), ptr(self.states), hs), "stft_ola_gated")
         return True
+
+    def _pipelined_pass(self, marks=None) -> bool:
+        """One pipelined pass into the other output buffer, limiting the
+        pending one inside the launch; False (nothing launched) when the
+        library declines the shape (then pipelining stays off)."""
+        L, hs = lib(), stream_handle()
+        nxt = 1 - self._cur
+        prev_y = self._ys[self._cur] if self.pending else None
+        prev_pk = self._pks[self._cur] if self.pending else None
+        self._pks[nxt].zero_()
+        if marks:
+            marks[0].record()
+        rc = L.tomatis_stft_ola_gated_pipelined(
+            self.plan.h, ptr(self.ss.x), ptr(self.gains), self.n_rows, ptr(self._ys[nxt]),
+            ptr(self._pks[nxt]), PEAK_LIMIT, ptr(self.r), ptr(self.states), ptr(prev_y),
+            ptr(prev_pk), hs)
+        if rc == E_UNSUPPORTED:
+            self.pipelined = False
+            return False
+        check(rc, "stft_ola_gated_pipelined")
+        self._cur = nxt
+        self.y, self.peaks = self._ys[nxt], self._pks[nxt]
+        self.pending = True
+        return True
+
+    def flush(self):
+        """Pipelined: apply the limiter to the last pass's output (it has no
+        next pass to do it); no-op otherwise."""
+        if self.pending:
+            check(lib().tomatis_apply_limiter(self.plan.h, ptr(self.y), ptr(self.peaks),
+                                              PEAK_LIMIT, stream_handle()), "apply_limiter")
+            self.pending = False
 
     def _two_pass(self, marks=None):
         L, P, hs = lib(), self.plan.h, stream_handle()
@@ -542,8 +592,11 @@ class GatePipeline:
         gate carry re-runs the pass on the two-pass chain (same results)."""
         if self.gated_used:
             def redo_gate():
+                # (a pipelined launch limited the previous output whatever its
+                # own gate did; this pass is recomputed, limited, into self.y)
                 self.gated_used = False
                 self.gate_fallbacks += 1
+                self.pending = False
                 self._two_pass()
             # a limiter-wait redo of the gated pass: the transform alone cannot
             # recompute states, so the two-pass chain runs with the unfused limiter
@@ -551,6 +604,7 @@ class GatePipeline:
         return finish_plan(self.plan, self._transform, "GatePipeline")
 
     def result(self) -> Result:
+        self.flush()
         st = self.streams
         return Result(y=self.y, out_offs=self.out_offs, out_lens=[s.out_len for s in st],
                       ch=self.ss.ch, frame_base=[s.frame_base for s in st],
