@@ -40,6 +40,11 @@ WORKLOADS = {
            "gate_ui 50 (log_percent)"),
     "c4": (64, 300, 48000, 2, "standard", 2048, 512,
            "C4: 64 x 5 min stereo 48 kHz per GPU (512 over 8 GPUs), standard, 2048/512"),
+    # C4 with stream 17 a sine hovering at the gate threshold for all 5 minutes
+    # (every run of it chains its look-back: no two-pass fallback)
+    "c4h": (64, 300, 48000, 2, "standard", 2048, 512,
+            "C4 + one hovering stream: 64 x 5 min stereo 48 kHz per GPU, stream 17 a "
+            "1 kHz sine at the gate threshold (-40 dBFS), standard, 2048/512"),
     "c5x": (16, 300, 96000, 2, "xfade", 4096, 1024,
             "C5 stage 1: 16 x 5 min stereo 96 kHz per GPU, xfade 500 ms, 4096/1024"),
     "c3": (64, 300, 44100, 2, "adaptive", 2048, 512,
@@ -152,6 +157,57 @@ def _pool_task(args):
     return time.perf_counter() - t0
 
 
+def _file_task(args):
+    """The CPU file -> file path for one FLAC PCM_24 file in a worker process
+    (one thread, codec included): host FLAC decode -> the oracle's
+    process_standard (levels, gate, STFT filter, OLA, per-chunk limiter) ->
+    PCM_24 quantisation + host FLAC encode -> write; the reference's own file
+    path, src/process_tomatis.py:225-251,433-457, with the package's codec in
+    place of libsndfile (absent here)."""
+    src, dst, n_fft, hop = args
+    os.environ["TOMATIS_FLAC_THREADS"] = "1"
+    from oracle import tomatis_oracle as orc
+    from tomatis_audio_processor_amd import audio_io
+    t0 = time.perf_counter()
+    x, sr = audio_io.read(src)
+    ref = orc.process_standard(x, sr, gate_ui=50, n_fft=n_fft, hop=hop)
+    audio_io.write(dst, ref["y"], sr, "FLAC", "PCM_24")
+    return time.perf_counter() - t0
+
+
+def cpu_file_baseline(file_s: int, sr: int, n_fft: int, hop: int, ch: int):
+    """CPU file -> file (BASELINE.md §4.5's separate end-to-end number): FLAC
+    PCM_24 files of ``file_s`` s (seeds 1000..; written by the host codec
+    before timing), one process on one core, then P = host cores processes
+    with one file each (aggregate = all channel-samples / the slowest worker).
+    The GPU's file -> file rate is tools/bench_file.py's."""
+    import multiprocessing as mp
+    import tempfile
+    from tomatis_audio_processor_amd import audio_io
+    from tomatis_audio_processor_amd.synth import synth_stream
+    P = _host_cores()
+    n = file_s * sr
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as d:
+        srcs = []
+        for i in range(P):
+            f = os.path.join(d, f"in{i}.flac")
+            audio_io.write(f, synth_stream(1000 + i, n, ch, sr), sr, "FLAC", "PCM_24")
+            srcs.append(f)
+        dt1 = _file_task((srcs[0], os.path.join(d, "one.flac"), n_fft, hop))
+        pool_val = None
+        if P > 1:
+            tasks = [(f, os.path.join(d, f"out{i}.flac"), n_fft, hop) for i, f in enumerate(srcs)]
+            with mp.get_context("spawn").Pool(P) as pool:
+                dts = pool.map(_file_task, tasks, chunksize=1)
+            pool_val = round(P * n * ch / max(dts) / 1e6, 3)
+    return {"value": pool_val if pool_val is not None else round(n * ch / dt1 / 1e6, 3),
+            "unit": "Msamples/s", "cores": P if pool_val is not None else 1,
+            "single_core": round(n * ch / dt1 / 1e6, 3),
+            "sample": f"{P} FLAC PCM_24 files of {file_s} s stereo {sr} Hz: host FLAC decode -> "
+                      f"oracle process_standard -> PCM_24 FLAC encode -> write, one thread per "
+                      f"process ({P} processes, one file each); single_core: one of them alone"}
+
+
 def cpu_baseline(sample_s: int, sr: int, n_fft: int, hop: int, ch: int, x_host=None,
                  pool_s: int = 300):
     """The oracle (a 'port' of the reference loop) on the host:
@@ -228,6 +284,8 @@ def main():
                          "PMC traffic runs)")
     ap.add_argument("--cpu-pool-s", type=int, default=300,
                     help="seconds of audio per worker for the all-cores CPU baseline")
+    ap.add_argument("--cpu-file-s", type=int, default=120,
+                    help="seconds per FLAC file of the CPU file->file baseline (0 disables)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="standard mode: every pass applies its own limiter (no batch "
                          "pipeline: tomatis_stft_ola_gated instead of _pipelined)")
@@ -265,6 +323,11 @@ def main():
         ss = engine.StreamSet.synthetic(nstr, n, ch, sr, seed0=1000 + rank * nstr)
         if a.input_gain != 1.0:
             ss.x = engine.scale_copy(ss.x, a.input_gain)
+        if a.workload == "c4h":
+            o, amp = ss.offs[17], np.sqrt(2.0) * 10.0 ** (-40.0 / 20.0)
+            t = torch.arange(n, dtype=torch.float64, device="cuda") / sr
+            s = (amp * torch.sin(2 * np.pi * 1000.0 * t)).to(torch.float32)
+            ss.x[o:o + 2 * n] = torch.stack([s, s], 1).reshape(-1)
     stages = 1
     if mode == "standard":
         # batch pipeline: pass k+1's transform applies pass k's limiter in its
@@ -344,6 +407,8 @@ def main():
         if a.cpu_sample_s > 0 and mode == "standard" and not strong:
             xs = ss.x[:a.cpu_sample_s * sr * ch].cpu().numpy().reshape(-1, ch)
             cpu = cpu_baseline(a.cpu_sample_s, sr, n_fft, hop, ch, x_host=xs, pool_s=a.cpu_pool_s)
+            if a.cpu_file_s > 0:
+                cpu["file_to_file"] = cpu_file_baseline(a.cpu_file_s, sr, n_fft, hop, ch)
         out = {
             "metric": "Msamples/s (44.1 kHz stereo) end-to-end STFT-gate-OLA; % HBM roofline",
             "value": round(value, 1), "unit": "Msamples/s", "n_gpus": ws, "steps": a.steps,
@@ -358,6 +423,7 @@ def main():
                                        f"file-parallel x{ws} (RCCL manifest all_gather)"),
                        "fused_levels": bool(getattr(pipe, "gated_used", False)),
                        "pipelined": bool(getattr(pipe, "pipelined", False)),
+                       "gate_fallbacks": int(getattr(pipe, "gate_fallbacks", 0)),
                        **({"dev_overrides": a.dev} if a.dev else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -7,8 +7,9 @@ The fused kernel computes every frame's r from the samples it loads for the FFT
 via dsp.frame_rms) and steps the gate automaton (:377-385) from the state a
 look-back pre-kernel found before its run; r, states, output and chunk peaks
 must equal the two-pass chain bit for bit.  A stream whose level hovers inside
-the hysteresis band for more than the look-back leaves runs unresolved: the
-pass is flagged (TOMATIS_ERR_GATE_CARRY) and re-run on the two-pass chain.
+the hysteresis band chains its runs' carries (k_gate_chain); only runs that
+cannot chain stay unresolved: the pass is flagged (TOMATIS_ERR_GATE_CARRY) and
+re-run on the two-pass chain.
 """
 import numpy as np
 import pytest
@@ -25,6 +26,11 @@ def _engine():
         pytest.skip("no GPU")
     from tomatis_audio_processor_amd import engine
     return torch, engine
+
+
+def _dev_opts(**kw):
+    from tomatis_audio_processor_amd._lib import dev_options
+    return dev_options(**kw)
 
 
 def _pair(E, ss, **kw):
@@ -135,34 +141,86 @@ def test_gated_vs_oracle():
     assert err <= 1e-4, err
 
 
-def test_gated_fallback_hovering_level():
-    """A sine whose level sits at the gate threshold T (inside the +-1.5 dB
-    hysteresis band: neither "on" nor "off") for ~1400 frames: every run that
-    starts more than 512 frames after the stream's quiet first frame finds no
-    state-fixing frame in its look-back.  The pass must be flagged and re-run on
-    the two-pass chain, with the two-pass results; a loud stream in the same
+def _hover(n, sr, T=-40.0):
+    """a stereo sine whose level sits at the gate threshold T (gate_ui 50,
+    log_percent: inside the +-1.5 dB hysteresis band, neither "on" nor "off")"""
+    amp = np.sqrt(2.0) * 10.0 ** (T / 20.0)
+    s = (amp * np.sin(2 * np.pi * 1000.0 * np.arange(n) / sr)).astype(np.float32)
+    return np.stack([s, s], 1)
+
+
+def test_gated_chained_hovering_level():
+    """A level hovering inside the hysteresis band for ~1400 frames: no run
+    after the quiet first frame finds a state-fixing frame, so each run's
+    look-back stops at the previous run's first frame and chains (its transfer
+    function over the frames between, composed in run order by k_gate_chain).
+    No fallback; bit-identical to the two-pass chain; a loud stream in the same
     batch is unaffected."""
     torch, E = _engine()
     sr, hop = 44100, 512
     n = hop * 1400
-    T = -40.0  # gate_ui 50, log_percent
-    amp = np.sqrt(2.0) * 10.0 ** (T / 20.0)
-    t = np.arange(n) / sr
-    s = (amp * np.sin(2 * np.pi * 1000.0 * t)).astype(np.float32)
-    hover = np.stack([s, s], 1)
-    loud = synth_stream(8, n, 2, sr)
-    ss = E.StreamSet.from_arrays([hover, loud], sr)
-    pipe, ref = _pair(E, ss, gate_ui=50, n_fft=2048, hop=hop)
+    ss = E.StreamSet.from_arrays([_hover(n, sr), synth_stream(8, n, 2, sr)], sr)
+    with _dev_opts(RUN_FRAMES=48):  # many runs: long chains of chained runs
+        pipe, ref = _pair(E, ss, gate_ui=50, n_fft=2048, hop=hop)
+    assert pipe.gated_used and pipe.gate_fallbacks == 0
+    _assert_same(torch, pipe, ref)
+    st = pipe.result().stream_states(0)
+    assert (st == 1).all()  # stays C1 after its quiet start (never D + 1 frames on)
+
+
+def test_gated_fallback_unchainable():
+    """Chaining needs up_delay_frames + 2 <= 1024 transfer-table states; with a
+    longer up-delay a hovering stream's runs stay unresolved after 512 frames of
+    look-back: the pass is flagged and re-run on the two-pass chain, with the
+    two-pass results, and the next run() tries the fused gate again."""
+    torch, E = _engine()
+    sr, hop = 44100, 256
+    n = hop * 2400
+    ud = 1100 * hop / sr * 1000.0  # 1100 frames of up-delay
+    ss = E.StreamSet.from_arrays([_hover(n, sr), synth_stream(8, n, 2, sr)], sr)
+    pipe, ref = _pair(E, ss, gate_ui=50, n_fft=2048, hop=hop, up_delay_ms=ud)
+    assert pipe.up_delay_frames + 2 > 1024
     assert pipe.gate_fallbacks == 1, "the unresolved carry must re-run the pass"
     assert not pipe.gated_used
     _assert_same(torch, pipe, ref)
-    # the hovering stream stays in C1 after its quiet start (never D + 1 frames on)
-    st = pipe.result().stream_states(0)
-    assert (st == 1).all()
-    # next run: the plan tries the fused gate again (the flag is per pass)
     pipe.run()
     assert pipe.gate_fallbacks == 2
     _assert_same(torch, pipe, ref)
+
+
+def test_gated_hovering_stream_in_c4_batch():
+    """BASELINE C4 as benched per GPU (64 x 5 min stereo 48 kHz) with one stream
+    hovering at the threshold for all 5 minutes: every run of it chains, the
+    pass takes the fused gate (no fallback), equals the two-pass chain bit for
+    bit, and costs about what a clean batch does."""
+    torch, E = _engine()
+    sr = 48000
+    n = 300 * sr
+    ss = E.StreamSet.synthetic(64, n, 2, sr, seed0=1000)
+    clean = E.GatePipeline(ss, gate_ui=50, n_fft=2048, hop=512)
+
+    def timed(pipe, k=4):
+        pipe.run()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record()
+        for _ in range(k):
+            pipe.run(check_device=False)
+        ev[1].record()
+        torch.cuda.synchronize()
+        return ev[0].elapsed_time(ev[1]) / k
+
+    t_clean = timed(clean)
+    del clean
+    o = ss.offs[17]
+    ss.x[o:o + 2 * n] = torch.from_numpy(_hover(n, sr).reshape(-1)).to(ss.x.device)
+    pipe, ref = _pair(E, ss, gate_ui=50, n_fft=2048, hop=512)
+    assert pipe.gated_used and pipe.gate_fallbacks == 0
+    _assert_same(torch, pipe, ref)
+    t_hover = timed(pipe)
+    assert pipe.gate_fallbacks == 0
+    # (the look-back of the hovering stream's runs walks their whole span once;
+    # a whole-batch two-pass re-run would double the pass)
+    assert t_hover <= 1.3 * t_clean, (t_hover, t_clean)
 
 
 def test_gated_declines_other_shapes():

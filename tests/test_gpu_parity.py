@@ -212,12 +212,15 @@ def test_gate_api_functions():
     assert st == ["C1" if s == 1 else "C2" for s in ref["states"]]
 
 
-@pytest.mark.parametrize("gate_path", ["runscan", "tf"])
+@pytest.mark.parametrize("gate_path", ["runscan", "tf", "fused"])
 @pytest.mark.parametrize("up_delay_ms", [0.0, 30.0, 250.0])
 def test_gate_paths_multistream(gate_path, up_delay_ms, monkeypatch):
-    """Both gate implementations (closed-form run scan, transfer-function scan)
-    against the reference automaton over the GPU's own frame r, on 3 streams of
-    different lengths whose level toggles around the thresholds every few frames."""
+    """Every gate implementation -- the two-pass chain's closed-form run scan
+    and transfer-function scan (tomatis_gate_std, fused_levels=False: they also
+    serve every gate-carry fallback, non-exclusive predicates and xfade) and the
+    in-kernel automaton (tomatis_stft_ola_gated) -- against the reference
+    automaton over the GPU's own frame r, on 3 streams of different lengths
+    whose level toggles around the thresholds every few frames."""
     torch, E = _engine()
     from oracle import tomatis_oracle as orc
     from tomatis_audio_processor_amd._lib import dev_options
@@ -228,9 +231,11 @@ def test_gate_paths_multistream(gate_path, up_delay_ms, monkeypatch):
         xs.append((rng.standard_normal((n, 2)) * steps[:, None]).astype(np.float32))
     ss = E.StreamSet.from_arrays(xs, sr)
     with dev_options(GATE_TF=1 if gate_path == "tf" else -1):
-        pipe = E.GatePipeline(ss, gate_ui=50, n_fft=2048, hop=512, up_delay_ms=up_delay_ms)
+        pipe = E.GatePipeline(ss, gate_ui=50, n_fft=2048, hop=512, up_delay_ms=up_delay_ms,
+                              fused_levels=gate_path == "fused")
         res = pipe.run()
         torch.cuda.synchronize()
+    assert pipe.gated_used == (gate_path == "fused")
     for i in range(3):
         r = res.stream_r(i)
         starts = res.first_start[i] + 512 * np.arange(len(r), dtype=np.int64)

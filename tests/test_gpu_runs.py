@@ -6,7 +6,10 @@ The host cuts every stream into interior runs (fast loop) and edge runs
 launch.  Every output hop block is the same frame-ordered float32 sum whatever
 the cut, so outputs, chunk peaks and states must be bitwise identical across:
 run lengths (TOMATIS_DEV_RUN_FRAMES), the interior loop on/off
-(TOMATIS_DEV_FAST_LOOP), and the fused/unfused limiter (TOMATIS_DEV_FUSE_LIMITER).  One small case is also
+(TOMATIS_DEV_FAST_LOOP), and the fused/unfused limiter (TOMATIS_DEV_FUSE_LIMITER),
+for the two-pass chain (tomatis_levels -> tomatis_gate_std -> transform) and,
+at n_fft 2048 / hop 512, the in-kernel gate (tomatis_stft_ola_gated) as well,
+which must also agree with each other.  One small case is also
 checked against the oracle.  Streams of unequal, odd lengths make frame_base
 odd for some streams (the gain-row ids are read as aligned 32-bit words).
 """
@@ -32,11 +35,12 @@ def _dev(env):
     return dev_options(**{k.replace("TOMATIS_", ""): int(v) for k, v in env.items()})
 
 
-def _run(E, torch, xs, sr, env, **params):
+def _run(E, torch, xs, sr, env, fused=False, **params):
     with _dev(env):
         ss = E.StreamSet.from_arrays(xs, sr)
-        pipe = E.GatePipeline(ss, **params)
+        pipe = E.GatePipeline(ss, fused_levels=fused, **params)
         res = pipe.run()
+        assert pipe.gated_used == (fused and params["n_fft"] == 2048 and params["hop"] == 512)
         torch.cuda.synchronize()
         pipe.plan.check_device()
         outs = [res.output(i) for i in range(len(xs))]
@@ -56,8 +60,12 @@ def test_decomposition_bit_identical(n_fft, hop, sr):
     variants = [{"TOMATIS_RUN_FRAMES": 48}, {"TOMATIS_RUN_FRAMES": 131},
                 {"TOMATIS_RUN_FRAMES": 1000}, {"TOMATIS_FAST_LOOP": 0},
                 {"TOMATIS_FUSE_LIMITER": 0}, {"TOMATIS_RUN_FRAMES": 77, "TOMATIS_FUSE_LIMITER": 0}]
-    for env in variants:
-        got = _run(E, torch, xs, sr, env, **params)
+    runs = [(env, False) for env in variants]
+    if n_fft == 2048 and hop == 512:  # the in-kernel gate takes this shape
+        runs += [({}, True), ({"TOMATIS_RUN_FRAMES": 131}, True), ({"TOMATIS_RUN_FRAMES": 1000}, True),
+                 ({"TOMATIS_FUSE_LIMITER": 0}, True)]
+    for env, fused in runs:
+        got = _run(E, torch, xs, sr, env, fused=fused, **params)
         for i in range(len(xs)):
             assert np.array_equal(got[1][i], base[1][i]), (env, i, "states")
             assert got[2][i].tobytes() == base[2][i].tobytes(), (env, i, "chunk peaks")

@@ -1655,6 +1655,12 @@ struct tomatis_plan_s {
   int32_t* gate_carry = nullptr;
   float* gate_win = nullptr;
   int gate_cap = 0;
+  uint16_t* gate_tf = nullptr;     // chained runs' transfer tables [gate_cap][D + 2]
+  int32_t* run_first = nullptr;    // per stream: first run index (n_streams + 1)
+  // the look-back the carries in gate_carry belong to (input, run layout)
+  const float* gl_x = nullptr;
+  int gl_gen = -1;
+  int runs_gen = 0;                // bumped whenever build_runs re-lays the runs
   // run-scan gate (exclusive on/off predicates)
   bool gate_excl = false;
   void* gsum = nullptr;
@@ -1742,6 +1748,7 @@ int tomatis_plan_destroy(tomatis_plan_t p) {
                   p->aq, p->afin, p->acin,
                   p->chunk_need, p->chunk_done, p->chunk_rng, p->err, p->twL,
                   p->partner, p->chunk_final, p->pieces, p->xs_pieces, p->gate_carry, p->gate_win,
+                  p->gate_tf, p->run_first,
                   p->pw_leaf, p->pw_prog, p->blue_b, p->blue_h, p->glb_work};
   for (void* q : ptrs) dfree(q);
   delete p;
@@ -1887,6 +1894,15 @@ static int build_runs(tomatis_plan_s* p) {
   p->runs = nullptr;
   if ((rc = dalloc_copy(&p->runs, runs))) return rc;
   p->hruns = runs;
+  ++p->runs_gen;  // carries of an earlier look-back no longer match these runs
+  {  // first run of every stream (runs are in stream order)
+    std::vector<int32_t> rf(ns + 1, (int32_t)runs.size());
+    for (int i = (int)runs.size() - 1; i >= 0; --i) rf[runs[i].s] = i;
+    for (int st = ns - 1; st >= 0; --st) rf[st] = std::min(rf[st], rf[st + 1]);
+    dfree(p->run_first);
+    p->run_first = nullptr;
+    if ((rc = dalloc_copy(&p->run_first, rf))) return rc;
+  }
   p->n1 = 0;
   if (two) {  // round 1 = the first half of the runs (stream / position order)
     p->n1 = p->n_runs / 2;
@@ -2591,17 +2607,26 @@ struct GateOut {
 
 // per-run carry-in state id and leaf window of the fused gate (k_gate_carry)
 static int gate_lookback(tomatis_plan_s* p, const float* x, hipStream_t s) {
+  const int nst = p->d.up_delay_frames + 2;
+  const bool chain = nst <= kGateChainStates;
   if (p->n_runs > p->gate_cap) {
     dfree(p->gate_carry);
     dfree(p->gate_win);
+    dfree(p->gate_tf);
     p->gate_carry = nullptr;
     p->gate_win = nullptr;
+    p->gate_tf = nullptr;
     p->gate_cap = 0;
     if (hipMalloc(reinterpret_cast<void**>(&p->gate_carry), (size_t)p->n_runs * sizeof(int32_t)) ||
         hipMalloc(reinterpret_cast<void**>(&p->gate_win), (size_t)p->n_runs * 16 * sizeof(float)))
       return TOMATIS_E_NOMEM;
+    if (chain && hipMalloc(reinterpret_cast<void**>(&p->gate_tf),
+                           (size_t)p->n_runs * nst * sizeof(uint16_t)))
+      return TOMATIS_E_NOMEM;
     p->gate_cap = p->n_runs;
   }
+  p->gl_x = x;
+  p->gl_gen = p->runs_gen;
   if (p->n_runs == 0) return TOMATIS_OK;
   MainArgs A{};
   A.x = x;
@@ -2612,7 +2637,8 @@ static int gate_lookback(tomatis_plan_s* p, const float* x, hipStream_t s) {
   A.hop = p->d.hop;
   A.ch = p->d.ch;
   A.gate_D = p->d.up_delay_frames;
-  launch_gate_carry(A, p->P, p->SH, p->d.ch, p->gate_carry, p->gate_win, s);
+  launch_gate_carry(A, p->P, p->SH, p->d.ch, p->gate_carry, p->gate_win,
+                    chain ? p->gate_tf : nullptr, p->run_first, p->n_streams, s);
   return launch_check();
 }
 
@@ -2747,7 +2773,9 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
   if (gate) {
     // per run: the carry-in state id and leaf window (k_gate_carry), then the
     // transform computes every frame's r and state from the input it loads
-    if (!gate->lookback_done || p->n_runs > p->gate_cap) {
+    // (re-run a look-back made for another input or run layout: the caller's
+    // tomatis_gate_lookback must match this call, the ABI does not assume it)
+    if (!gate->lookback_done || p->n_runs > p->gate_cap || p->gl_x != x || p->gl_gen != p->runs_gen) {
       const int rc = gate_lookback(p, x, s);
       if (rc) return rc;
     }

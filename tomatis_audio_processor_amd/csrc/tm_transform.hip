@@ -1010,12 +1010,22 @@ __global__ __launch_bounds__(64) void k_r2_plan(MainArgs A, const uint32_t* __re
 // run is left unresolved, carry = -1, and the host falls back to the two-pass
 // path); the state then runs forward over the recorded predicates to kf.
 // Blocks are prefetched 4 ahead.
+// Chained runs: a look-back that reaches kc, the first frame of the previous
+// run of the same stream, without an anchor needs no more frames -- the state
+// before kf is the state before kc (that run's own carry-in) stepped over the
+// predicates of frames [kc, kf), which the walk has recorded.  The run then
+// stores the automaton's transfer function over those frames (one lane per
+// start state: tf[run][s], s < nst = D + 2) and carry = kGateChained;
+// k_gate_chain composes the carries in run order afterwards.  Only a run whose
+// look-back exceeds kGateLookbackMax frames (or nst > kGateChainStates) stays
+// unresolved (carry -1: the host's two-pass fallback).
 template <int CH, int SH>
 __global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restrict__ carry,
-                                                   float* __restrict__ win) {
+                                                   float* __restrict__ win,
+                                                   uint16_t* __restrict__ tf) {
   constexpr int P = 64, NR = 32, HOP = SH * P, NB = NR / SH, LB = SH / 2, PFD = 4;
   __shared__ __attribute__((aligned(16))) float scr[LB * kLvLS];
-  __shared__ uint8_t prs[kGateLookback];
+  __shared__ uint8_t prs[kGateLookbackMax];
   const int run = blockIdx.x;
   if (run >= A.n_runs) return;
   const int L = threadIdx.x;
@@ -1023,6 +1033,13 @@ __global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restri
   const TomatisStream S = A.st[R.s];
   const int D = A.gate_D;
   const int64_t kf = max<int64_t>(0, R.ka - (A.rmax - 1));
+  // chain point: the first frame of the previous run of this stream (runs are
+  // in stream / frame order); 0 for a stream's first run (the stream start
+  // anchors it).  Without a tf table the walk keeps the kGateLookback limit.
+  int64_t kc = 0;
+  if (run > 0 && A.runs[run - 1].s == R.s) kc = max<int64_t>(0, A.runs[run - 1].ka - (A.rmax - 1));
+  const bool can_chain = tf != nullptr && kc > 0 && kf - kc <= kGateLookbackMax;
+  const int cap = can_chain ? kGateLookbackMax : kGateLookback;
   const __amdgpu_buffer_rsrc_t rx =
       mk_rsrc(A.x + S.in_off, (uint32_t)min<int64_t>(S.n * CH * 4, 0x7fffffffll));
   auto load_block = [&](int64_t b, cf (&dst)[SH]) {  // block b of the frame grid
@@ -1108,7 +1125,10 @@ __global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restri
                 a_k = -1;
                 a_id = 0;
                 go = false;
-              } else if (n >= kGateLookback) {
+              } else if (can_chain && j == kc) {
+                a_k = -3;  // chained: frames [kc, kf) recorded
+                go = false;
+              } else if (n >= cap) {
                 exact = true;  // let the exact walk decide (and flag) this run
                 go = false;
               } else {
@@ -1152,7 +1172,10 @@ __global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restri
             a_k = -1;  // stream start: C1 idle before frame 0
             a_id = 0;
             more = false;
-          } else if (n >= kGateLookback) {
+          } else if (can_chain && j == kc) {
+            a_k = -3;  // chained: frames [kc, kf) recorded
+            more = false;
+          } else if (n >= cap) {
             more = false;  // unresolved
           } else {
             lw = lv_window<SH, false>(lw, lv_leaves<CH, SH, SH>(bq[u], scr, L));
@@ -1167,12 +1190,44 @@ __global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restri
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (a_k == -2) {
       id = -1;
+    } else if (a_k == -3) {
+      // transfer function over frames [kc, kf): lane s replays from state s
+      const int nst = D + 2;
+      for (int s0 = 0; s0 < nst; s0 += 64) {
+        int t = s0 + L;
+        for (int64_t k = kc; k < kf; ++k) t = gate_step(t, prs[kf - 1 - k], D);
+        if (s0 + L < nst) tf[(int64_t)run * nst + s0 + L] = (uint16_t)t;
+      }
+      id = kGateChained;
     } else {
       id = a_id;
       for (int64_t k = a_k + 1; k < kf; ++k) id = gate_step(id, prs[kf - 1 - k], D);
     }
   }
   if (L == 0) carry[run] = id;
+}
+
+// Chained carries in run order, one lane per stream: a chained run's carry is
+// its transfer function applied to the previous run's carry (resolved, or
+// itself chained and composed just before); an unresolved predecessor leaves
+// it unresolved.
+__global__ __launch_bounds__(64) void k_gate_chain(const Run* __restrict__ runs, int n_runs,
+                                                   const int32_t* __restrict__ run_first,
+                                                   int n_streams, int nst,
+                                                   int32_t* __restrict__ carry,
+                                                   const uint16_t* __restrict__ tf) {
+  const int s = blockIdx.x * 64 + threadIdx.x;
+  if (s >= n_streams) return;
+  const int r1 = run_first[s + 1];
+  int prev = -1;
+  for (int r = run_first[s]; r < r1 && r < n_runs; ++r) {
+    int c = carry[r];
+    if (c == kGateChained) {
+      c = prev < 0 ? -1 : (int)tf[(int64_t)r * nst + prev];
+      carry[r] = c;
+    }
+    prev = c;
+  }
 }
 
 // Generic hop: same transform, windowed frame outputs to scratch, then a gather.
@@ -1689,16 +1744,21 @@ void launch_r2_plan(const MainArgs& A, const uint32_t* chunk_final, uint32_t* pi
 }
 
 void launch_gate_carry(const MainArgs& A, int P, int SH, int ch, int32_t* gcarry, float* gwin,
-                       hipStream_t s) {
+                       uint16_t* gtf, const int32_t* run_first, int n_streams, hipStream_t s) {
   if (A.n_runs <= 0 || P != 64) return;
   const dim3 g(A.n_runs), b(64);
   if (SH == 8) {
-    if (ch == 2) hipLaunchKernelGGL((k_gate_carry<2, 8>), g, b, 0, s, A, gcarry, gwin);
-    else hipLaunchKernelGGL((k_gate_carry<1, 8>), g, b, 0, s, A, gcarry, gwin);
+    if (ch == 2) hipLaunchKernelGGL((k_gate_carry<2, 8>), g, b, 0, s, A, gcarry, gwin, gtf);
+    else hipLaunchKernelGGL((k_gate_carry<1, 8>), g, b, 0, s, A, gcarry, gwin, gtf);
   } else if (SH == 4) {
-    if (ch == 2) hipLaunchKernelGGL((k_gate_carry<2, 4>), g, b, 0, s, A, gcarry, gwin);
-    else hipLaunchKernelGGL((k_gate_carry<1, 4>), g, b, 0, s, A, gcarry, gwin);
+    if (ch == 2) hipLaunchKernelGGL((k_gate_carry<2, 4>), g, b, 0, s, A, gcarry, gwin, gtf);
+    else hipLaunchKernelGGL((k_gate_carry<1, 4>), g, b, 0, s, A, gcarry, gwin, gtf);
+  } else {
+    return;
   }
+  if (gtf && run_first && n_streams > 0)
+    hipLaunchKernelGGL(k_gate_chain, dim3((n_streams + 63) / 64), dim3(64), 0, s, A.runs, A.n_runs,
+                       run_first, n_streams, A.gate_D + 2, gcarry, gtf);
 }
 
 void launch_lds_gather(const LdsArgs& A, hipStream_t s) {

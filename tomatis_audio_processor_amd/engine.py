@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import threading
 import time
 import warnings
 from dataclasses import dataclass, field
@@ -240,7 +241,7 @@ def _levels_threaded(r: np.ndarray, out: np.ndarray, tmp: np.ndarray = None):
     dt = np.asarray(r).dtype
     if tmp is None or len(tmp) < n or tmp.dtype != dt:
         tmp = np.empty(n, dt)
-    k = int(os.environ.get("TOMATIS_LOG10_THREADS", "1"))
+    k = min(int(os.environ.get("TOMATIS_LOG10_THREADS", "1")), 16, os.cpu_count() or 1)
 
     def part(a, b):
         np.add(r[a:b], dsp.EPS, out=tmp[a:b])
@@ -258,15 +259,18 @@ def _levels_threaded(r: np.ndarray, out: np.ndarray, tmp: np.ndarray = None):
 
 
 _SLICE_POOL = None
+_SLICE_LOCK = threading.Lock()
 
 
 def _slice_pool(k: int):
     """Workers for the log10 slices of _levels_threaded only (never the pool
-    its callers run on)."""
+    its callers run on): one executor of fixed size (min(16, CPUs)), created
+    once under a lock; callers cap their slice count at its size."""
     global _SLICE_POOL
-    if _SLICE_POOL is None or _SLICE_POOL._max_workers < k:
-        import concurrent.futures as cf
-        _SLICE_POOL = cf.ThreadPoolExecutor(max_workers=max(1, min(16, k)))
+    with _SLICE_LOCK:
+        if _SLICE_POOL is None:
+            import concurrent.futures as cf
+            _SLICE_POOL = cf.ThreadPoolExecutor(max_workers=max(1, min(16, os.cpu_count() or 1)))
     return _SLICE_POOL
 
 
