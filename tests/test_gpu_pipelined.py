@@ -113,12 +113,14 @@ def test_pipelined_ragged():
 
 
 def test_pipelined_gate_fallback():
-    """Pass 1's input hovers at the gate threshold (look-back unresolved): that
-    pass is redone on the two-pass chain, limited; pass 0 was limited by pass
-    1's launch all the same, and pass 2 pipelines again from pass 1."""
+    """Pass 1's input hovers at the gate threshold with an up-delay too long to
+    chain look-backs (1100 frames: more than 1022 transfer-table states), so
+    its runs stay unresolved: that pass is redone on the two-pass chain,
+    limited; pass 0 was limited by pass 1's launch all the same, and pass 2
+    pipelines again (from nothing pending)."""
     torch, E = _engine()
-    sr, hop = 44100, 512
-    n = hop * 1400
+    sr, hop = 44100, 256
+    n = hop * 2400
     amp = np.sqrt(2.0) * 10.0 ** (-40.0 / 20.0)
     s = (amp * np.sin(2 * np.pi * 1000.0 * np.arange(n) / sr)).astype(np.float32)
     hover = np.stack([s, s], 1)
@@ -126,7 +128,7 @@ def test_pipelined_gate_fallback():
     arrays = [[loud[0], loud[1]], [hover, loud[1]], [loud[2], loud[0]]]
     ss = E.StreamSet.from_arrays(arrays[0], sr)
     xs = [E.StreamSet.from_arrays(a, sr).x.clone() for a in arrays]
-    kw = dict(gate_ui=50, n_fft=2048, hop=hop)
+    kw = dict(gate_ui=50, n_fft=2048, hop=hop, up_delay_ms=1100 * hop / sr * 1000.0)
     two = E.GatePipeline(ss, fused_levels=False, **kw)
     refs = []
     for x in xs:
