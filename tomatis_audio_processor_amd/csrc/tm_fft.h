@@ -386,17 +386,26 @@ __device__ __forceinline__ void xchg32(cf (&v)[32], float* buf, int L) {
 }
 #undef TM_ADDTID8
 
-// forward: v[n2] = x[L + 64 n2] -> bin layout above.  twN: the step-2 table
-// (lane-pair layout, as fft_fwd); w: W_64^{L & 31}.
-__device__ __forceinline__ void fftx_fwd(cf (&v)[32], int L, const cf* twN, cf w, float* buf) {
-  constexpr int P = 64, NR = 32;
+// step 1 + step 2 of the forward (P lanes: twN is [NR/2][P] lane pairs)
+// (P = 128: register 0 of wave 1 holds k2 = 16, whose twiddle is not 1)
+template <int P>
+__device__ __forceinline__ void fftx_head(cf (&v)[32], int L, const cf* twN) {
+  constexpr int NR = 32;
   sdft<NR, 0, 0, NR>(v);
   sfor<0, NR / 2>([&](auto kk) {
     constexpr int K2 = decltype(kk)::value;
     const float4 t = reinterpret_cast<const float4*>(twN)[K2 * P + L];
-    if constexpr (K2 > 0) v[2 * K2] = cmul(v[2 * K2], cf{t.x, t.y});
+    if constexpr (K2 > 0 || P > 64) v[2 * K2] = cmul(v[2 * K2], cf{t.x, t.y});
     v[2 * K2 + 1] = cmul(v[2 * K2 + 1], cf{t.z, t.w});
   });
+}
+// the 64-point DFT over the wave's lanes of each of the 32 registers (lane
+// bit 5 by permlane32 + butterfly, then the transpose and DFT_32): register r
+// of lane l -> lane (r', s) (r' = l & 31, s = l >> 5) register i holds
+// output k1 = (r' & 1) + 2 i of the DFT of register r = 2 (r' >> 1) + s.
+// l5: this lane's index within the wave (L & 63); w: W_64^{l5 & 31}
+__device__ __forceinline__ void fftx_tail(cf (&v)[32], int l5, cf w, float* buf) {
+  constexpr int NR = 32;
   sfor<0, NR / 2>([&](auto jj) {
     constexpr int J = decltype(jj)::value;
     swap32(v[2 * J], v[2 * J + 1]);
@@ -404,15 +413,14 @@ __device__ __forceinline__ void fftx_fwd(cf (&v)[32], int L, const cf* twN, cf w
     v[2 * J] = a + b;
     v[2 * J + 1] = cmul(a - b, w);
   });
-  xchg32(v, buf, L);
+  xchg32(v, buf, l5);
   sdft<NR, 0, 0, NR>(v);
 }
-
-// inverse (unnormalised): bin layout -> v[n2] = N x[L + 64 n2] / (sig1[L & 31] sig2[n2])
-__device__ __forceinline__ void fftx_inv(cf (&v)[32], int L, const cf* twN, cf w, float* buf) {
-  constexpr int P = 64, NR = 32;
+// inverse of fftx_tail (unnormalised); the outputs carry splan<32, 1>().sig[l5 & 31]
+__device__ __forceinline__ void fftx_itail(cf (&v)[32], int l5, cf w, float* buf) {
+  constexpr int NR = 32;
   sdft<NR, 1, 0, NR>(v);
-  xchg32(v, buf, L);
+  xchg32(v, buf, l5);
   sfor<0, NR / 2>([&](auto jj) {
     constexpr int J = decltype(jj)::value;
     const cf z0 = v[2 * J], z1 = cmulc(v[2 * J + 1], w);
@@ -420,19 +428,120 @@ __device__ __forceinline__ void fftx_inv(cf (&v)[32], int L, const cf* twN, cf w
     v[2 * J + 1] = z0 - z1;
     swap32(v[2 * J], v[2 * J + 1]);
   });
+}
+// inverse of fftx_head: conj step 2, then DFT_32 (plan 2) over k2 -> n2
+template <int P>
+__device__ __forceinline__ void fftx_ihead(cf (&v)[32], int L, const cf* twN) {
+  constexpr int NR = 32;
   sfor<0, NR / 2>([&](auto kk) {
     constexpr int K2 = decltype(kk)::value;
     const float4 t = reinterpret_cast<const float4*>(twN)[K2 * P + L];
-    if constexpr (K2 > 0) v[2 * K2] = cmulc(v[2 * K2], cf{t.x, t.y});
+    if constexpr (K2 > 0 || P > 64) v[2 * K2] = cmulc(v[2 * K2], cf{t.x, t.y});
     v[2 * K2 + 1] = cmulc(v[2 * K2 + 1], cf{t.z, t.w});
   });
   sdft<NR, 2, 0, NR>(v);
+}
+
+// forward: v[n2] = x[L + 64 n2] -> bin layout above.  twN: the step-2 table
+// (lane-pair layout, as fft_fwd); w: W_64^{L & 31}.
+__device__ __forceinline__ void fftx_fwd(cf (&v)[32], int L, const cf* twN, cf w, float* buf) {
+  fftx_head<64>(v, L, twN);
+  fftx_tail(v, L, w, buf);
+}
+
+// inverse (unnormalised): bin layout -> v[n2] = N x[L + 64 n2] / (sig1[L & 31] sig2[n2])
+__device__ __forceinline__ void fftx_inv(cf (&v)[32], int L, const cf* twN, cf w, float* buf) {
+  fftx_itail(v, L, w, buf);
+  fftx_ihead<64>(v, L, twN);
 }
 
 // bin index held by lane L, register i after fftx_fwd
 __device__ __forceinline__ int fftx_bin(int L, int i) {
   const int r = L & 31, s = L >> 5;
   return (2 * (r >> 1) + s) + 32 * (r & 1) + 64 * i;
+}
+
+// ---------------------------------------------------------------------------
+// n_fft 4096 on two waves (P = 128 lanes L = l + 64 w, 32 registers: sample
+// L + 128 n2).  Steps 1-2 as above per lane; the 128-point DFT over L = m + 64 w
+// starts with the radix-2 stage over the wave bit: wave w keeps k2 in
+// [16 w, 16 w + 16) and trades the other half with its partner through LDS
+// (8 KB each way, one pair barrier).  Wave 1 works with its k2 rotated by 16
+// (register r holds k2 = (r + 16) mod 32): its analysis window carries
+// (-1)^n2 (DFT_32 of x (-1)^n2 is X[k2 + 16]), its step-2 table row r the
+// twiddle of that k2, its synthesis window (-1)^n2 again -- so both waves send
+// registers 16..31 and receive into them, with no wave-dependent register
+// index.  After the trade register j holds Y[m, k2] and 16 + j holds
+// Y[m + 64, k2] in wave 0, the reverse in wave 1 (k2 = 16 w + j), so the
+// butterfly U_0 = v[j] + v[16 + j], U_1 = (v[j] - v[16 + j]) W_128^m takes
+// -W_128^m in wave 1 (twiddle table s_twP: W_128^{l} (1 - 2 w)).  Then each
+// wave runs fftx_tail's 64-point DFT over m on its 32 registers (j, 16 + j:
+// e = 0, 1).  Bin of lane L (w, l: r' = l & 31, s = l >> 5), register i:
+// r = 2 (r' >> 1) + s, k = (16 w + (r & 15)) + 32 (r >> 4) + 64 ((r' & 1) + 2 i).
+// LDS: two kXBuf-float regions H_0, H_1 (+ the pair-barrier counter).  Wave w
+// sends through its own region H_w and then runs its exchanges in H_{1-w};
+// on the way back it sends through H_{1-w}: no region is written while the
+// partner may still read it, with two pair barriers per frame.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void x128_trade(cf (&v)[32], int l, float* out, const float* in,
+                                           uint32_t* ctr, uint32_t* err) {
+  float2* o = reinterpret_cast<float2*>(out) + l;
+  const float2* q = reinterpret_cast<const float2*>(in) + l;
+  sfor<0, 16>([&](auto jj) {
+    constexpr int J = decltype(jj)::value;
+    o[64 * J] = make_float2(v[16 + J].x, v[16 + J].y);
+  });
+  pair_barrier(ctr, err);
+  sfor<0, 16>([&](auto jj) {
+    constexpr int J = decltype(jj)::value;
+    const float2 t = q[64 * J];
+    v[16 + J] = {t.x, t.y};
+  });
+}
+
+// forward.  buf: the sequence's 2 kXBuf regions (H_0, H_1) then the counter;
+// w128: W_128^{l} (1 - 2 w) (l = L & 63); w64: W_64^{l & 31}
+__device__ __forceinline__ void fftx128_fwd(cf (&v)[32], int L, const cf* twN, cf w128, cf w64,
+                                            float* buf, uint32_t* err) {
+  const int l = L & 63, w = __builtin_amdgcn_readfirstlane(L >> 6);
+  uint32_t* ctr = reinterpret_cast<uint32_t*>(buf + 2 * kXBuf);
+  float* const hw = buf + w * kXBuf;
+  float* const ho = buf + (1 - w) * kXBuf;
+  fftx_head<128>(v, L, twN);
+  x128_trade(v, l, hw, ho, ctr, err);
+  sfor<0, 16>([&](auto jj) {
+    constexpr int J = decltype(jj)::value;
+    const cf a = v[J], b = v[16 + J];
+    v[J] = a + b;
+    v[16 + J] = cmul(a - b, w128);
+  });
+  fftx_tail(v, l, w64, ho);
+}
+
+// inverse: bin layout -> v[n2] = N x[L + 128 n2] (-1)^{w n2} / (sig1[l & 31] sig2[n2])
+__device__ __forceinline__ void fftx128_inv(cf (&v)[32], int L, const cf* twN, cf w128, cf w64,
+                                            float* buf, uint32_t* err) {
+  const int l = L & 63, w = __builtin_amdgcn_readfirstlane(L >> 6);
+  uint32_t* ctr = reinterpret_cast<uint32_t*>(buf + 2 * kXBuf);
+  float* const hw = buf + w * kXBuf;
+  float* const ho = buf + (1 - w) * kXBuf;
+  fftx_itail(v, l, w64, ho);
+  // wave 0: v[j] = b 0 (kept), v[16 + j] = b 1 (wave 1's register 16 + j);
+  // wave 1 (twiddle negated): v[j] = b 1 (kept), v[16 + j] = b 0 (wave 0's)
+  sfor<0, 16>([&](auto jj) {
+    constexpr int J = decltype(jj)::value;
+    const cf z0 = v[J], z1 = cmulc(v[16 + J], w128);
+    v[J] = z0 + z1;
+    v[16 + J] = z0 - z1;
+  });
+  x128_trade(v, l, ho, hw, ctr, err);
+  fftx_ihead<128>(v, L, twN);
+}
+
+__device__ __forceinline__ int fftx128_bin(int L, int i) {
+  const int w = L >> 6, l = L & 63, rp = l & 31, s = l >> 5;
+  const int r = 2 * (rp >> 1) + s;
+  return (16 * w + (r & 15)) + 32 * (r >> 4) + 64 * ((rp & 1) + 2 * i);
 }
 
 // per-lane register tables (window, gains, 1/wsum) in lane-quad layout:

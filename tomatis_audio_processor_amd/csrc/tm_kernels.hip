@@ -2108,18 +2108,26 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
       // inverse's (whose inputs carry 1 / the forward's)
       const double* sigF = NRr == 32 ? splan<32, 0>().sig : splan<16, 0>().sig;
       const double* sigI = NRr == 32 ? splan<32, 2>().sig : splan<16, 2>().sig;
+      // n_fft 4096 single-exchange FFT (tm_fft.h fftx128_*): wave 1 (lanes >= 64)
+      // holds k2 rotated by 16 in register r: its step-2 row r twiddles
+      // k2 = (r + 16) mod 32, and both its windows carry (-1)^n2
+      const bool fx = p->fx, rot = fx && P == 128;
       std::vector<cf> twN((size_t)NRr * P), twP(P);
-      for (int k2 = 0; k2 < NRr; ++k2)
+      for (int r = 0; r < NRr; ++r)
         for (int n1 = 0; n1 < P; ++n1) {
+          const int k2 = (rot && n1 >= 64) ? (r + 16) % 32 : r;
           const double ang = -2.0 * M_PI * (double)((int64_t)n1 * k2 % N) / (double)N;
-          twN[((size_t)(k2 >> 1) * P + n1) * 2 + (k2 & 1)] = {(float)(cos(ang) * sigF[k2]),
-                                                             (float)(sin(ang) * sigF[k2])};
+          twN[((size_t)(r >> 1) * P + n1) * 2 + (r & 1)] = {(float)(cos(ang) * sigF[r]),
+                                                           (float)(sin(ang) * sigF[r])};
         }
       std::vector<float> winS(N);
-      // single-exchange FFT (tm_fft.h fftx_inv): lane m's first-DFT output scale too
-      const bool fx = p->fx;
-      for (int t = 0; t < N; ++t)
-        winS[t] = (float)((double)w[t] * sigI[t / P] * (fx ? splan<32, 1>().sig[(t % P) & 31] : 1.0));
+      // single-exchange FFTs (fftx_inv / fftx128_inv): lane m's first-DFT output scale too
+      for (int t = 0; t < N; ++t) {
+        const double sgn = (rot && (t % P) >= 64 && ((t / P) & 1)) ? -1.0 : 1.0;
+        winS[t] = (float)(sgn * (double)w[t] * sigI[t / P] *
+                          (fx ? splan<32, 1>().sig[(t % P) & 31] : 1.0));
+        if (rot && sgn < 0) w[t] = -w[t];  // analysis window (w2 / winv are built above)
+      }
       for (int m = 0; m < P; ++m) {
         const double ang = -2.0 * M_PI * (double)m / (double)P;
         twP[m] = {(float)cos(ang), (float)sin(ang)};
@@ -2299,7 +2307,7 @@ int tomatis_plan_create(tomatis_plan_t* out, const TomatisPlanDesc* desc, const 
       p->generic = true;  // chunk boundaries not on emit blocks: per-sample gather path
   }
   // n_fft 2048 fused kernels: the single-exchange FFT (its bin layout and scales)
-  p->fx = kFftX && !p->generic && p->P == 64 && p->NR == 32;
+  p->fx = kFftX && !p->generic && (p->P == 64 || p->P == 128) && p->NR == 32;
   int64_t fb = 0;
   int32_t cb = 0;
   for (int i = 0; i < n_streams; ++i) {

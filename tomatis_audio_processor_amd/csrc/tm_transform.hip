@@ -364,14 +364,21 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   constexpr int HOP = SH * P;
   constexpr int NC = NR - SH;  // carried accumulator registers
   constexpr int SHQ = (SH + 3) & ~3;  // winv registers padded to a quad
-  constexpr bool FX = kFftX && P == 64 && NR == 32;  // single-exchange FFT (tm_fft.h fftx_*)
+  // single-exchange FFTs (tm_fft.h fftx_*): one wave per frame at n_fft 2048,
+  // two at 4096 (fftx128_*: one cross-wave trade per direction)
+  constexpr bool FX = kFftX && P == 64 && NR == 32;
+  constexpr bool FX2 = kFftX && P == 128 && NR == 32;
+  // per sequence: FX one wave's exchange rows; FX2 two waves' rows + the pair
+  // counter (cf units)
+  constexpr int SEQ_CF = FX ? kXBuf / 2 : (FX2 ? kXBuf + 2 : G::SEQ_LDS);
+  constexpr int CTR_CF = FX2 ? kXBuf : G::BUF;  // pair-barrier counter slot
   constexpr bool LT = P == 64 && !FX;  // per-lane step-3 twiddle table
   __shared__ __attribute__((aligned(16))) cf s_twN[NR * P];
   __shared__ __attribute__((aligned(16))) cf s_twP[LT ? 8 * P : P];
   __shared__ __attribute__((aligned(16))) float s_win[N];      // lane-quad layout
   __shared__ __attribute__((aligned(16))) float s_winS[N];     // synthesis, scaled
   __shared__ __attribute__((aligned(16))) float s_winv[SHQ * P];  // lane-quad layout
-  __shared__ __attribute__((aligned(16))) cf s_buf[NSEQ][FX ? kXBuf / 2 : G::SEQ_LDS];
+  __shared__ __attribute__((aligned(16))) cf s_buf[NSEQ][SEQ_CF];
   __shared__ __attribute__((aligned(16))) float s_gain[GM ? 2 * N : 4];
   // PR: one hop block per sequence for the partner rescale (LDS-DMA target)
   __shared__ __attribute__((aligned(16))) char s_pbuf[PR ? NSEQ * SH * P * CH * 4 : 16];
@@ -380,6 +387,11 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
     for (int i = threadIdx.x; i < 8 * P; i += WG) {
       const int m = 2 * (i / (2 * P)) + (i & 1), l = (i / 2) % P;
       s_twP[i] = cscale(A.twP[((l & 7) * m) & (P - 1)], sig_at<8>(m));
+    }
+  } else if constexpr (FX2) {  // W_128^{l} (1 - 2 w): wave 1's butterflies are mirrored
+    for (int i = threadIdx.x; i < P; i += WG) {
+      const cf t = A.twP[i & 63];
+      s_twP[i] = (i < 64) ? t : cf{-t.x, -t.y};
     }
   } else {
     for (int i = threadIdx.x; i < P; i += WG) s_twP[i] = A.twP[i];
@@ -401,7 +413,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       s_gain[i] = A.gains[(int64_t)A.lds_row[i >= N] * N + (i >= N ? i - N : i)];
   }
   if constexpr (P > 64) {  // pair-barrier counters (tm_fft.h)
-    if (threadIdx.x < NSEQ) reinterpret_cast<uint32_t*>(s_buf[threadIdx.x] + G::BUF)[0] = 0u;
+    if (threadIdx.x < NSEQ) reinterpret_cast<uint32_t*>(s_buf[threadIdx.x] + CTR_CF)[0] = 0u;
   }
   __syncthreads();
   const float4* const w4 = reinterpret_cast<const float4*>(s_win);
@@ -515,6 +527,8 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       }
       TPROF(1, v[NR - 1].x);
       if constexpr (FX) fftx_fwd(v, L, s_twN, s_twP[L & 31], reinterpret_cast<float*>(buf));
+      else if constexpr (FX2)
+        fftx128_fwd(v, L, s_twN, s_twP[L], s_twP[2 * (L & 31)], reinterpret_cast<float*>(buf), A.err);
       else fft_fwd<P, NR, LT>(v, L, s_twN, s_twP, buf, A.err);
       TPROF(2, v[NR - 1].x);
       // ---- gain row (real, even, 1/N folded in), per-lane layout ----
@@ -544,6 +558,8 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       }
       TPROF(3, v[NR - 1].x);
       if constexpr (FX) fftx_inv(v, L, s_twN, s_twP[L & 31], reinterpret_cast<float*>(buf));
+      else if constexpr (FX2)
+        fftx128_inv(v, L, s_twN, s_twP[L], s_twP[2 * (L & 31)], reinterpret_cast<float*>(buf), A.err);
       else fft_inv<P, NR, LT>(v, L, s_twN, s_twP, buf, A.err);
       TPROF(4, v[NR - 1].x);
       // ---- synthesis window (x the inverse FFT's output scales) + register OLA ----
@@ -1305,7 +1321,7 @@ __global__ void k_gain_perm(const float* __restrict__ g, int n_rows, int n_bins,
   if (t >= n_rows * N) return;
   const int row = t / N, e = t - row * N;  // e = lq(i, L)
   const int q = e >> 2, L = q % P, i = (q / P) * 4 + (e & 3);
-  int b = FX ? fftx_bin(L, i) : fft_bin<P, NR>(L, i);
+  int b = !FX ? fft_bin<P, NR>(L, i) : (P == 64 ? fftx_bin(L, i) : fftx128_bin(L, i));
   b = (b <= N / 2) ? b : N - b;
   // x the forward FFT's output scale of register i (its last DFT's output)
   out[t] = (g[(int64_t)row * n_bins + b] * (1.0f / (float)N)) * (FX ? sig_at<32>(i) : sig_at<8>(i & 7));
@@ -1711,6 +1727,8 @@ void launch_gain_perm(int P, int NR, bool fx, const float* gains, int n_rows, in
   const int nb = (n_rows * N + 255) / 256;
   if (P == 64 && fx)
     hipLaunchKernelGGL((k_gain_perm<64, 32, true>), dim3(nb), dim3(256), 0, s, gains, n_rows, n_bins, out);
+  else if (P == 128 && NR == 32 && fx)
+    hipLaunchKernelGGL((k_gain_perm<128, 32, true>), dim3(nb), dim3(256), 0, s, gains, n_rows, n_bins, out);
   else if (P == 64)
     hipLaunchKernelGGL((k_gain_perm<64, 32>), dim3(nb), dim3(256), 0, s, gains, n_rows, n_bins, out);
   else if (NR == 16)
