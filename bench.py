@@ -287,8 +287,8 @@ def main():
     ap.add_argument("--cpu-file-s", type=int, default=120,
                     help="seconds per FLAC file of the CPU file->file baseline (0 disables)")
     ap.add_argument("--no-pipeline", action="store_true",
-                    help="standard mode: every pass applies its own limiter (no batch "
-                         "pipeline: tomatis_stft_ola_gated instead of _pipelined)")
+                    help="standard / adaptive: every pass applies its own limiter (no batch "
+                         "pipeline: tomatis_stft_ola_gated / _limited instead of _pipelined)")
     ap.add_argument("--dev", action="append", default=[], metavar="NAME=VALUE",
                     help="development override (TOMATIS_DEV_<NAME>, A/B experiments); "
                          "recorded in the JSON line's config")
@@ -339,8 +339,10 @@ def main():
                                    xfade_ms=500.0)
     elif mode == "adaptive":
         # two stream groups: one group's host phase overlaps the other's device work
+        # (batch pipeline as in standard mode: the global limiter of pass k in
+        # pass k+1's transforms)
         pipe = engine.AdaptiveGroups(ss, groups=int(os.environ.get("TOMATIS_C3_GROUPS", "2")),
-                                     n_fft=n_fft, hop=hop)
+                                     n_fft=n_fft, hop=hop, pipelined=not a.no_pipeline)
     elif mode == "chain":
         pipe = ChainC5(engine, ss, sr, n_fft, hop)
         stages = 2

@@ -62,7 +62,7 @@
 extern "C" {
 #endif
 
-#define TOMATIS_ABI_VERSION 7
+#define TOMATIS_ABI_VERSION 8
 
 #define TOMATIS_OK 0
 #define TOMATIS_E_ARG (-1)        /* bad argument */
@@ -285,6 +285,17 @@ int tomatis_stft_ola_gated_pipelined(tomatis_plan_t plan, const float* x,
                                      uint32_t* chunk_peak_bits, float limit, float* r_out,
                                      uint8_t* states_out, float* prev_y,
                                      const uint32_t* prev_peak_bits, void* hip_stream);
+/* The same batch pipeline for the two-pass chain (gain-row ids from the
+ * caller: the adaptive processor's min-hold states, src/process_tomatis_adaptive.py
+ * :298-345, whose global limiter is one chunk per stream): as
+ * tomatis_stft_ola_limited except that y is left unscaled and prev_y (the
+ * previous call's output with this plan, peaks prev_peak_bits) is limited
+ * inside this launch.  TOMATIS_E_UNSUPPORTED unless n_fft 2048, hop <= 512
+ * (hop 512 for cross-fade row tables) and limiter chunks exist. */
+int tomatis_stft_ola_pipelined(tomatis_plan_t plan, const float* x, const float* gain_rows,
+                               int32_t n_rows, const uint16_t* rows, float* y,
+                               uint32_t* chunk_peak_bits, float limit, float* prev_y,
+                               const uint32_t* prev_peak_bits, void* hip_stream);
 /* The limiter on the edge chunks of edge_mask only. */
 int tomatis_apply_limiter_edges(tomatis_plan_t plan, float* y, const uint32_t* chunk_peak_bits,
                                 float limit, int32_t edge_mask, void* hip_stream);

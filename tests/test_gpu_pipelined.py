@@ -160,3 +160,52 @@ def test_pipelined_declines():
         pipe = E.GatePipeline(ss, gate_ui=50, pipelined=True, **kw)
         res = pipe.run()
         assert res is not None and not pipe.pending, kw
+
+
+@pytest.mark.parametrize("groups", [1, 2])
+def test_pipelined_adaptive(groups):
+    """Adaptive batches (AdaptiveGroups, src/process_tomatis_adaptive.py): the
+    global limiter of pass k applied inside pass k+1's transforms
+    (tomatis_stft_ola_pipelined), a different input per pass (attenuation and
+    threshold change): output, global peaks, states and alpha bit-identical to
+    unpipelined passes."""
+    torch, E = _engine()
+    sr, ns, n = 44100, 6, 44100 * 40 + 391
+    xs = _inputs(E, torch, ns, n, 2, sr, [1.0, 0.3, 1.0, 0.05, 0.6, 1.0], 3)
+    ss = E.StreamSet.synthetic(ns, n, 2, sr, seed0=1)
+    kw = dict(n_fft=2048, hop=512)
+    ref = E.AdaptiveGroups(ss, groups=groups, **kw)
+    refs = []
+    for x in xs:
+        ss.x.copy_(x)
+        res = ref.run()
+        refs.append((res.y.clone(), res.chunk_peaks.clone(), res.states.clone(), res.alpha.clone()))
+    del ref
+    pipe = E.AdaptiveGroups(ss, groups=groups, pipelined=True, **kw)
+    held = None
+    for k, x in enumerate(xs):
+        ss.x.copy_(x)
+        assert pipe.run() is None and pipe.pending and pipe.pipelined
+        if held is not None:
+            y, pk, st, al = held
+            torch.cuda.synchronize()
+            assert torch.equal(st, refs[k - 1][2]) and torch.equal(al, refs[k - 1][3])
+            assert torch.equal(pk, refs[k - 1][1]), f"pass {k - 1}: peaks differ"
+            assert torch.equal(y, refs[k - 1][0]), f"pass {k - 1}: output differs"
+        # the result's arrays of this pass (y: the buffer, final after the next pass)
+        r = E.merge_results([Result_nf(p) for p in pipe.pipes])
+        held = (r.y, r.chunk_peaks.clone(), r.states.clone(), r.alpha.clone())
+    res = pipe.result()
+    assert not pipe.pending
+    assert torch.equal(res.chunk_peaks, refs[-1][1])
+    assert torch.equal(res.y, refs[-1][0])
+
+
+def Result_nf(p):
+    """a pipeline's Result without flushing (its arrays as they stand)"""
+    pend = p.pending
+    p.pending = False
+    try:
+        return p.result()
+    finally:
+        p.pending = pend

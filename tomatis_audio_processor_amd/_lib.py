@@ -14,7 +14,7 @@ import ctypes as C
 import os
 
 LIB_NAME = "libtomatis_hip.so"
-ABI_VERSION = 7  # include/tomatis_hip.h TOMATIS_ABI_VERSION
+ABI_VERSION = 8  # include/tomatis_hip.h TOMATIS_ABI_VERSION
 GATE_SEGMENT = 1024      # TOMATIS_GATE_SEGMENT
 GATE_NONE = -536870912   # TOMATIS_GATE_NONE
 ERR_LIMITER_WAIT = 1     # TOMATIS_ERR_LIMITER_WAIT
@@ -114,6 +114,8 @@ _SIGS = {
                                                         _P, _P, _P]),
     "tomatis_stft_ola_gated_pipelined": (C.c_int, [_P, _P, _P, C.c_int32, _P, _P, C.c_float,
                                                    _P, _P, _P, _P, _P]),
+    "tomatis_stft_ola_pipelined": (C.c_int, [_P, _P, _P, C.c_int32, _P, _P, _P, C.c_float,
+                                             _P, _P, _P]),
     "tomatis_ts_summary": (C.c_int, [_P, _P, C.c_int32, C.c_int32, _P, _P]),
     "tomatis_ts_gate": (C.c_int, [_P, _P, _P, C.c_int32, C.c_int32, _P, _P, _P]),
     "tomatis_plan_error": (C.c_int, [_P, _P]),

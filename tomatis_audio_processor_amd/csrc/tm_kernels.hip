@@ -2983,6 +2983,25 @@ int tomatis_stft_ola_gated_pipelined(tomatis_plan_t p, const float* x, const flo
   return stft_ola_impl(p, x, gains, n_rows, nullptr, y, peaks, limit, hs, &g, &pb);
 }
 
+int tomatis_stft_ola_pipelined(tomatis_plan_t p, const float* x, const float* gains,
+                               int32_t n_rows, const uint16_t* rows, float* y, uint32_t* peaks,
+                               float limit, float* prev_y, const uint32_t* prev_peaks, void* hs) {
+  if (!p || !x || !gains || !rows || !y || !peaks || n_rows < 1 || !(limit > 0.f) ||
+      (prev_y && (!prev_peaks || prev_y == y || prev_peaks == peaks)))
+    return TOMATIS_E_ARG;
+  // the partner-rescale instantiations: n_fft 2048 interior loop, hop <= 512,
+  // gain rows in LDS (one or two rows; the cross-fade lattice's pure rows at
+  // hop 512), per-chunk accounting
+  const TomatisPlanDesc& d = p->d;
+  const bool lds_rows = n_rows <= 2 ||
+                        (d.alpha_mode != 0 && p->SH == 8 && dev_opt(TOMATIS_DEV_GAIN_LDS, 1) != 0);
+  if (p->generic || p->lds || p->P != 64 || p->NR != 32 || p->SH > 8 || !lds_rows ||
+      p->total_chunks <= 0 || !p->chunk_need)
+    return TOMATIS_E_UNSUPPORTED;
+  const PrevBatch pb{prev_y, prev_peaks};
+  return stft_ola_impl(p, x, gains, n_rows, rows, y, peaks, limit, hs, nullptr, &pb);
+}
+
 int tomatis_stft_ola_limited(tomatis_plan_t p, const float* x, const float* gains,
                              int32_t n_rows, const uint16_t* rows, float* y, uint32_t* peaks,
                              float limit, void* hs) {

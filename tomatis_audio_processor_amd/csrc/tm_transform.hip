@@ -1601,6 +1601,14 @@ void launch_main_pf(const MainArgs& A, int ch, hipStream_t s) {
   }
   if constexpr (P == 64 && WG == 512 && SH <= 8) {  // (LDS slots: host limits rounds to hop <= 512)
     if (A.partner || A.yprev) {  // round 2 / pipelined batch (two-row tables: gm == 1)
+      if constexpr (SH == 8) {
+        // pipelined adaptive batches (cross-fade lattice: the pure rows in LDS)
+        if (gm == 2) {
+          if (ch == 2) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 2, PF, NT, WG, true>), g, b, 0, s, A);
+          else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, 2, PF, NT, WG, true>), g, b, 0, s, A);
+          return;
+        }
+      }
       if (ch == 2) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 1, PF, NT, WG, true>), g, b, 0, s, A);
       else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, 1, PF, NT, WG, true>), g, b, 0, s, A);
       return;
@@ -1660,7 +1668,7 @@ void launch_main(const MainArgs& A, int ch, int wg, hipStream_t s) {
     if (wg == 768) return launch_main_pf<P, NR, SH, PF, true, 768>(A, ch, s);
     if (wg == 512) return launch_main_pf<P, NR, SH, PF, true, 512>(A, ch, s);
   }
-  launch_main_pf<P, NR, SH, PF, true, 256>(A, ch, s);
+  if constexpr (P != 64) launch_main_pf<P, NR, SH, PF, true, 256>(A, ch, s);
 }
 
 }  // namespace

@@ -647,9 +647,13 @@ class AdaptivePipeline:
 
     def __init__(self, ss: StreamSet, *, fc=1000.0, slope=12.0, c1_low=15.0, c1_high=-15.0,
                  c2_low=-15.0, c2_high=15.0, target_c2=0.5, hyst_db=3.0, min_hold_ms=250.0,
-                 xfade_ms=500.0, headroom_margin=2.0, n_fft=4096, hop=2048, out=None):
+                 xfade_ms=500.0, headroom_margin=2.0, n_fft=4096, hop=2048, out=None,
+                 pipelined=False, out2=None):
         """``out``: optional (y, offsets) output buffer shared with other
-        pipelines (AdaptiveGroups)."""
+        pipelines (AdaptiveGroups).  ``pipelined``: a batch pipeline as
+        GatePipeline's (tomatis_stft_ola_pipelined: each pass's transform
+        applies the previous pass's global limiter; ``out2`` the second output
+        buffer, same offsets, when ``out`` is shared)."""
         torch = _torch()
         _check_fft(n_fft, hop, ss.ch)
         self.ss, self.n_fft, self.hop = ss, n_fft, hop
@@ -707,6 +711,12 @@ class AdaptivePipeline:
         self.gains = torch.from_numpy(np.stack(rows)).to(dev)
         self.n_rows = len(rows)
         self.out_offs = out_offs
+        self.pipelined = bool(pipelined)
+        self.pending = False      # pipelined: self.y awaits its limiter
+        if self.pipelined:
+            self._ys = [self.y, out2 if out2 is not None else torch.empty_like(self.y)]
+            self._pks = [self.peaks, torch.zeros_like(self.peaks)]
+            self._cur = 0
 
     def run(self, marks=None, timer=None, check_device: bool = True):
         """``timer`` (a dict) collects synchronised wall-clock phases (profiling).
@@ -715,22 +725,61 @@ class AdaptivePipeline:
             pass
         if check_device:
             self.finish()
-        return self.result()
+        return None if self.pending else self.result()
 
     def _transform(self):
         """STFT-gain-OLA, normalise max(w,1e-8), restore, global limiter (one
-        chunk per stream: fused into the transform when its runs allow)"""
+        chunk per stream: fused into the transform when its runs allow;
+        pipelined: the previous pass's limiter inside this transform)"""
+        if self.pipelined and self._pipelined_pass():
+            return
+        self.flush()
+        self._limited()
+
+    def _limited(self):
         self.peaks.zero_()
         check(lib().tomatis_stft_ola_limited(self.plan.h, ptr(self.ss.x), ptr(self.gains),
                                              self.n_rows, ptr(self.rows), ptr(self.y),
                                              ptr(self.peaks), PEAK_LIMIT, stream_handle()),
               "stft_ola_limited")
 
+    def _pipelined_pass(self) -> bool:
+        nxt = 1 - self._cur
+        prev_y = self._ys[self._cur] if self.pending else None
+        prev_pk = self._pks[self._cur] if self.pending else None
+        self._pks[nxt].zero_()
+        rc = lib().tomatis_stft_ola_pipelined(
+            self.plan.h, ptr(self.ss.x), ptr(self.gains), self.n_rows, ptr(self.rows),
+            ptr(self._ys[nxt]), ptr(self._pks[nxt]), PEAK_LIMIT, ptr(prev_y), ptr(prev_pk),
+            stream_handle())
+        if rc == E_UNSUPPORTED:
+            self.pipelined = False
+            return False
+        check(rc, "stft_ola_pipelined")
+        self._cur = nxt
+        self.y, self.peaks = self._ys[nxt], self._pks[nxt]
+        self.pending = True
+        return True
+
+    def flush(self):
+        """Pipelined: the last pass's global limiter (on the pipeline's stream)."""
+        if self.pending:
+            torch = _torch()
+            with torch.cuda.stream(self.stream or torch.cuda.current_stream()):
+                check(lib().tomatis_apply_limiter(self.plan.h, ptr(self.y), ptr(self.peaks),
+                                                  PEAK_LIMIT, stream_handle()), "apply_limiter")
+            self.pending = False
+
     def finish(self) -> int:
-        """Device error check after the pass (on the pipeline's stream)."""
+        """Device error check after the pass (on the pipeline's stream); a
+        limiter-wait redo runs the transform unpipelined into the same buffer."""
         torch = _torch()
+
+        def redo():
+            self.pending = False
+            self._limited()
         with torch.cuda.stream(self.stream or torch.cuda.current_stream()):
-            return finish_plan(self.plan, self._transform, "AdaptivePipeline")
+            return finish_plan(self.plan, redo, "AdaptivePipeline")
 
     def steps(self, marks=None, timer=None, after=None):
         """The pass as a generator that yields wherever the host would wait for
@@ -869,6 +918,7 @@ class AdaptivePipeline:
         self.prec = prec
 
     def result(self) -> Result:
+        self.flush()
         st = list(self.plan.streams)[:self.ss.n_streams]
         return Result(y=self.y, out_offs=self.out_offs, out_lens=[s.out_len for s in st],
                       ch=self.ss.ch, frame_base=[s.frame_base for s in st],
@@ -928,12 +978,15 @@ class AdaptiveGroups:
     one: a fused-limiter launch never shares the dispatcher with another).
     Output in one buffer; ``result()`` merges the groups."""
 
-    def __init__(self, ss: StreamSet, groups: int = 2, **params):
+    def __init__(self, ss: StreamSet, groups: int = 2, pipelined=False, **params):
+        """``pipelined``: every group pipelines its passes (AdaptivePipeline);
+        the groups alternate between two shared output buffers in step."""
         torch = _torch()
         n_fft, hop = params.get("n_fft", 4096), params.get("hop", 2048)
         G = max(1, min(int(groups), ss.n_streams))
         out_lens = [N if dsp.adaptive_frames(N, n_fft, hop)[1] else 0 for N in ss.lens]
         self.y, offs = _alloc_out(torch, out_lens, ss.ch, ss.x.device)
+        y2 = torch.empty_like(self.y) if pipelined else None
         # contiguous groups balanced by samples
         tot, acc, cuts = float(sum(ss.lens)) or 1.0, 0, [0]
         for i, N in enumerate(ss.lens):
@@ -949,7 +1002,8 @@ class AdaptiveGroups:
         chain = os.environ.get("TOMATIS_C3_SYNC", "first") == "chain"
         for g, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
             sub = StreamSet(x=ss.x, offs=ss.offs[a:b], lens=ss.lens[a:b], ch=ss.ch, sr=ss.sr)
-            p = AdaptivePipeline(sub, out=(self.y, offs[a:b]), **params)
+            p = AdaptivePipeline(sub, out=(self.y, offs[a:b]), pipelined=pipelined, out2=y2,
+                                 **params)
             p.stream = torch.cuda.Stream()
             serial = mh_mode == "serial" or (mh_mode == "auto" and chain and g > 0)
             p.plan.set_option(OPT_MINHOLD_SERIAL, int(serial))
@@ -991,7 +1045,24 @@ class AdaptiveGroups:
             cur.wait_stream(p.stream)
         if check_device:
             self.finish()
-        return self.result()
+        return None if self.pending else self.result()
+
+    @property
+    def pending(self) -> bool:
+        return any(p.pending for p in self.pipes)
+
+    @property
+    def pipelined(self) -> bool:
+        return all(p.pipelined for p in self.pipes)
+
+    def flush(self):
+        """Pipelined: every group's last global limiter (then the current
+        stream waits for them)."""
+        torch = _torch()
+        cur = torch.cuda.current_stream()
+        for p in self.pipes:
+            p.flush()
+            cur.wait_stream(p.stream)
 
     def finish(self) -> int:
         bits = 0
@@ -1000,6 +1071,7 @@ class AdaptiveGroups:
         return bits
 
     def result(self) -> Result:
+        self.flush()
         return merge_results([p.result() for p in self.pipes])
 
 
