@@ -62,7 +62,7 @@
 extern "C" {
 #endif
 
-#define TOMATIS_ABI_VERSION 8
+#define TOMATIS_ABI_VERSION 9
 
 #define TOMATIS_OK 0
 #define TOMATIS_E_ARG (-1)        /* bad argument */
@@ -336,18 +336,12 @@ int tomatis_plan_error_bits(tomatis_plan_t plan, uint32_t* bits, int32_t reset,
  *       when every stream's tables fit the LDS (else serial); 1: the 30 steps
  *       in one workgroup per stream -- the small footprint to prefer when the
  *       call overlaps another stream group's transform.
- *   TOMATIS_OPT_LIMITER_ROUNDS (0 auto / 1 / 2): the fused limiter of
- *       standard-mode n_fft 2048 plans in two rounds (auto: one round): round 1
- *       leaves its output unscaled, round 2 scales it block by block inside its
- *       own frame loop, so only round 2's rescale is a tail.  Same results. */
+ * (Option 4, the two-round fused limiter of ABI <= 7, is withdrawn: the
+ * pipelined calls apply a batch's limiter inside the next batch's transform.) */
 #define TOMATIS_OPT_FUSE_LIMITER 1
 #define TOMATIS_OPT_LIMITER_SPIN 2
 #define TOMATIS_OPT_MINHOLD_SERIAL 3
-#define TOMATIS_OPT_LIMITER_ROUNDS 4
 int tomatis_plan_set_option(tomatis_plan_t plan, int32_t option, int64_t value);
-/* 2 when the plan's fused limiter runs in two rounds (TOMATIS_OPT_LIMITER_ROUNDS
- * auto/2 and an eligible plan), else 1; -1 for a null plan. */
-int32_t tomatis_plan_limiter_rounds(tomatis_plan_t plan);
 
 /* Development overrides (tests and A/B experiments only).  Process-wide,
  * explicit: the library reads no environment variable.  value < 0 restores the
@@ -355,8 +349,8 @@ int32_t tomatis_plan_limiter_rounds(tomatis_plan_t plan);
  * frame), FAST_LOOP (interior loop), RUN_FRAMES (frames per run, 0 auto),
  * RUN_ROUNDS, LEVELS_LEGACY, GATE_TF (transfer-function gate scan), MH_PARTS;
  * at launch: GATE_TF, ALPHA_SEQ (sequential xfade alpha), GAIN_LDS,
- * FUSE_LIMITER, WG (transform workgroup size), FUSED_LEVELS; LIMITER_ROUNDS at
- * plan creation.  Results are bit-identical
+ * FUSE_LIMITER, WG (transform workgroup size), FUSED_LEVELS (key 13 is
+ * unused).  Results are bit-identical
  * under every value (the decomposition tests vary them). */
 #define TOMATIS_DEV_FAST_LOOP 1
 #define TOMATIS_DEV_RUN_ROUNDS 2
@@ -370,7 +364,6 @@ int32_t tomatis_plan_limiter_rounds(tomatis_plan_t plan);
 #define TOMATIS_DEV_GAIN_LDS 10
 #define TOMATIS_DEV_FUSE_LIMITER 11
 #define TOMATIS_DEV_WG 12
-#define TOMATIS_DEV_LIMITER_ROUNDS 13  /* initial TOMATIS_OPT_LIMITER_ROUNDS of new plans */
 #define TOMATIS_DEV_FUSED_LEVELS 14    /* 0: tomatis_stft_ola_gated declines (host two-pass) */
 int tomatis_set_dev_option(int32_t key, int32_t value);
 /* The current override of key (-1: default, or an unknown key). */

@@ -14,7 +14,7 @@ import ctypes as C
 import os
 
 LIB_NAME = "libtomatis_hip.so"
-ABI_VERSION = 8  # include/tomatis_hip.h TOMATIS_ABI_VERSION
+ABI_VERSION = 9  # include/tomatis_hip.h TOMATIS_ABI_VERSION
 GATE_SEGMENT = 1024      # TOMATIS_GATE_SEGMENT
 GATE_NONE = -536870912   # TOMATIS_GATE_NONE
 ERR_LIMITER_WAIT = 1     # TOMATIS_ERR_LIMITER_WAIT
@@ -24,11 +24,10 @@ E_UNSUPPORTED = -2       # TOMATIS_E_UNSUPPORTED
 OPT_FUSE_LIMITER = 1     # TOMATIS_OPT_FUSE_LIMITER
 OPT_LIMITER_SPIN = 2     # TOMATIS_OPT_LIMITER_SPIN
 OPT_MINHOLD_SERIAL = 3   # TOMATIS_OPT_MINHOLD_SERIAL
-OPT_LIMITER_ROUNDS = 4   # TOMATIS_OPT_LIMITER_ROUNDS
 # development overrides (TOMATIS_DEV_*: tests and A/B experiments only)
 DEV_KEYS = dict(FAST_LOOP=1, RUN_ROUNDS=2, RUN_FRAMES=3, LEVELS_LEGACY=4, GATE_TF=5, MH_PARTS=6,
                 FORCE_LDS=7, P64=8, ALPHA_SEQ=9, GAIN_LDS=10, FUSE_LIMITER=11, WG=12,
-                LIMITER_ROUNDS=13, FUSED_LEVELS=14)
+                FUSED_LEVELS=14)
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 F32, F64 = 0, 1
@@ -121,7 +120,6 @@ _SIGS = {
     "tomatis_plan_error": (C.c_int, [_P, _P]),
     "tomatis_plan_error_bits": (C.c_int, [_P, C.POINTER(C.c_uint32), C.c_int32, _P]),
     "tomatis_plan_set_option": (C.c_int, [_P, C.c_int32, C.c_int64]),
-    "tomatis_plan_limiter_rounds": (C.c_int32, [_P]),
     "tomatis_set_dev_option": (C.c_int, [C.c_int32, C.c_int32]),
     "tomatis_get_dev_option": (C.c_int32, [C.c_int32]),
     "tomatis_absmax": (C.c_int, [_P, C.c_int64, _P, _P]),

@@ -1638,15 +1638,6 @@ struct tomatis_plan_s {
   int edge_mask = 0;      // set for one tomatis_stft_ola_limited_edges call
   int fuse_enabled = 1;   // TOMATIS_OPT_FUSE_LIMITER
   int lim_spin = 1 << 18; // TOMATIS_OPT_LIMITER_SPIN: fused-limiter wait bound (polls)
-  // two-round fused limiter (TOMATIS_OPT_LIMITER_ROUNDS): runs
-  // [0, n1) are round 1, [n1, n_runs) round 2; partner[r] = the round-1 run whose
-  // output round-2 run r scales; chunk_final[g] = no round-2 contributions
-  int lim_rounds = 0;     // option: 0 auto, 1 off, 2 on
-  int n1 = 0;             // > 0: the plan's runs are laid out for two rounds
-  int32_t* partner = nullptr;
-  uint32_t* chunk_final = nullptr;
-  uint32_t* pieces = nullptr;
-  int max_pieces = 0;
   // pipelined batches (tomatis_stft_ola_gated_pipelined): per run the previous
   // batch's blocks to rescale in the frame loop (k_r2_plan output)
   uint32_t* xs_pieces = nullptr;
@@ -1747,7 +1738,7 @@ int tomatis_plan_destroy(tomatis_plan_t p) {
                   p->grp_base, p->leaf_base, p->leaves, p->gsum, p->gcarry, p->gcarry_in,
                   p->aq, p->afin, p->acin,
                   p->chunk_need, p->chunk_done, p->chunk_rng, p->err, p->twL,
-                  p->partner, p->chunk_final, p->pieces, p->xs_pieces, p->gate_carry, p->gate_win,
+                  p->xs_pieces, p->gate_carry, p->gate_win,
                   p->gate_tf, p->run_first,
                   p->pw_leaf, p->pw_prog, p->blue_b, p->blue_h, p->glb_work};
   for (void* q : ptrs) dfree(q);
@@ -1776,20 +1767,13 @@ static bool gate_exclusive(const TomatisStream& S) {
   return true;
 }
 
-// Runs of the fused kernel (plan creation, and again when
-// TOMATIS_OPT_LIMITER_ROUNDS changes the layout), then the fused-limiter
-// accounting that depends on them.
+// Runs of the fused kernel (plan creation), then the fused-limiter accounting
+// that depends on them.
 static int build_runs(tomatis_plan_s* p) {
   const TomatisPlanDesc& d = p->d;
   const int N = d.n_fft, hop = d.hop, P = p->P;
   const int ns = p->n_streams;
   int rc;
-  // two-round fused limiter: standard-mode register plans (two gain rows, LDS),
-  // n_fft 2048 (the interior loop), when TOMATIS_OPT_LIMITER_ROUNDS asks for it
-  // (auto = one round: measured on C2, round 2's in-loop rescale hides 0.15 ms
-  // of tail but the split costs about as much -- DESIGN.md §6)
-  const bool two = !p->generic && P == 64 && d.alpha_mode == 0 && p->total_chunks > 0 &&
-                   p->lim_rounds == 2 && N <= 2048 && p->SH <= 8;  // (LDS slots: hop <= 512)
   const int64_t tf_total = std::max<int64_t>(1, p->total_frames);
   // Runs.  Per stream, the emitted frames [e_lo, e_hi) whose run can take the
   // fused kernel's interior loop (full frame loads back to the warm-up frames,
@@ -1843,7 +1827,7 @@ static int build_runs(tomatis_plan_s* p) {
   // runs still compute, and their limiter rescale overlaps that compute
   // (adaptive: every stream is one limiter chunk, measured 1.4 ms faster on C3
   // with 2 rounds; standard 10 s chunks gain nothing and pay warm-up frames)
-  const int rounds = std::max(1, dev_opt(TOMATIS_DEV_RUN_ROUNDS, (two || (d.alpha_mode == 2 && ns > 1)) ? 2 : 1));
+  const int rounds = std::max(1, dev_opt(TOMATIS_DEV_RUN_ROUNDS, (d.alpha_mode == 2 && ns > 1) ? 2 : 1));
   int T = dev_opt(TOMATIS_DEV_RUN_FRAMES, 0);
   if (T <= 0) {
     // generic streams and the edge runs take slots first
@@ -1903,18 +1887,12 @@ static int build_runs(tomatis_plan_s* p) {
     p->run_first = nullptr;
     if ((rc = dalloc_copy(&p->run_first, rf))) return rc;
   }
-  p->n1 = 0;
-  if (two) {  // round 1 = the first half of the runs (stream / position order)
-    p->n1 = p->n_runs / 2;
-    if (p->n1 == 0) p->n1 = 0;
-  }
   return TOMATIS_OK;
 }
 
 // Fused-limiter accounting over the plan's runs: flushes expected per chunk
-// (host mirror of the kernel's frame-indexed chunk walk), the largest run span
-// of a chunk, and for the two-round layout the partner of every round-2 run,
-// the chunks round 1 completes and the round-2 piece lists.
+// (host mirror of the kernel's frame-indexed chunk walk) and the largest run
+// span of a chunk.
 static int limiter_accounting(tomatis_plan_s* p) {
   if (p->generic || p->total_chunks <= 0) return TOMATIS_OK;
   const int HOP = p->d.hop, wpr = p->P / 64;
@@ -1957,32 +1935,9 @@ static int limiter_accounting(tomatis_plan_s* p) {
   dfree(p->chunk_need);
   p->chunk_need = nullptr;
   if ((rc = dalloc_copy(&p->chunk_need, need))) return rc;
-  dfree(p->partner);
-  dfree(p->chunk_final);
-  dfree(p->pieces);
-  p->partner = nullptr;
-  p->chunk_final = nullptr;
-  p->pieces = nullptr;
-  p->max_pieces = 0;
   dfree(p->xs_pieces);  // re-sized for these runs on the next pipelined batch
   p->xs_pieces = nullptr;
   p->xs_max_pieces = 0;
-  if (p->n1 > 0) {
-    const int nr = (int)runs.size(), n1 = p->n1, n2 = nr - n1;
-    std::vector<int32_t> partner(nr, -1);
-    for (int i = 0; i < n1 && i < n2; ++i) partner[n1 + i] = i;
-    std::vector<uint32_t> fin(p->total_chunks, 0);
-    for (int g = 0; g < p->total_chunks; ++g) fin[g] = (last_run[g] >= 0 && last_run[g] < n1) ? 1u : 0u;
-    int mp = 1;
-    for (int ri = n1; ri < nr; ++ri)
-      mp = std::max<int>(mp, (int)(runs[ri].kb - std::max<int64_t>(0, runs[ri].ka - (p->rmax - 1))));
-    p->max_pieces = mp;
-    if ((rc = dalloc_copy(&p->partner, partner))) return rc;
-    if ((rc = dalloc_copy(&p->chunk_final, fin))) return rc;
-    if (hipMalloc(reinterpret_cast<void**>(&p->pieces),
-                  (size_t)std::max(1, n2) * 2 * (mp + 1) * sizeof(uint32_t)))
-      return TOMATIS_E_NOMEM;
-  }
   return TOMATIS_OK;
 }
 
@@ -2281,7 +2236,6 @@ int tomatis_plan_create(tomatis_plan_t* out, const TomatisPlanDesc* desc, const 
   if (!p) return TOMATIS_E_NOMEM;
   p->d = d;
   p->n_streams = n_streams;
-  p->lim_rounds = std::max(0, std::min(2, dev_opt(TOMATIS_DEV_LIMITER_ROUNDS, 0)));
   const int N = d.n_fft, hop = d.hop;
   // (lanes P, registers NR) per transform: 2048 = 128 x 16, 4096 = 128 x 32
   // n_fft 2048: one wave per frame (P = 64, 32 registers, wave-local exchanges)
@@ -2767,7 +2721,6 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
   A.prof = nullptr;
   A.run_base = 0;
   A.defer_self = 0;
-  A.partner = nullptr;
   A.pieces = nullptr;
   A.max_pieces = 0;
   A.gated = 0;
@@ -2821,7 +2774,7 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
       A.peaks_prev = prev->peaks;
       A.pieces = p->xs_pieces;
       A.max_pieces = p->xs_max_pieces;
-      launch_r2_plan(A, nullptr, p->xs_pieces, s);
+      launch_r2_plan(A, p->xs_pieces, s);
       if ((rc = launch_check())) return rc;
     }
     launch_transform(A, p->P, p->NR, p->SH, ch, transform_wg(p->P, p->NR), s);
@@ -2847,28 +2800,6 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
   }
   return launch_check();
 #endif
-  // two-round fused limiter: round 1 leaves its output unscaled; k_r2_plan lists
-  // the round-1 blocks each round-2 run scales inside its frame loop (chunks
-  // complete after round 1); round 2 then runs with its partners (two-row LDS
-  // gain tables only, the kernel's GM 1 instantiation)
-  if (limit > 0.f && p->n1 > 0 && p->partner && A.n_rows_lds > 0 && !A.lds_mixed) {
-    MainArgs A1 = A;
-    A1.n_runs = p->n1;
-    A1.defer_self = 1;
-    launch_transform(A1, p->P, p->NR, p->SH, ch, transform_wg(p->P, p->NR), s);
-    int rc = launch_check();
-    if (rc) return rc;
-    MainArgs A2 = A;
-    A2.run_base = p->n1;
-    A2.n_runs = p->n_runs - p->n1;
-    A2.partner = p->partner;
-    A2.pieces = p->pieces;
-    A2.max_pieces = p->max_pieces;
-    launch_r2_plan(A2, p->chunk_final, p->pieces, s);
-    if ((rc = launch_check())) return rc;
-    launch_transform(A2, p->P, p->NR, p->SH, ch, transform_wg(p->P, p->NR), s);
-    return launch_check();
-  }
   launch_transform(A, p->P, p->NR, p->SH, ch, transform_wg(p->P, p->NR), s);
   return launch_check();
 }
@@ -3037,15 +2968,6 @@ int tomatis_plan_set_option(tomatis_plan_t p, int32_t option, int64_t value) {
       p->lim_spin = (int)value;
       return TOMATIS_OK;
     case TOMATIS_OPT_MINHOLD_SERIAL: p->mh_serial = value != 0; return TOMATIS_OK;
-    case TOMATIS_OPT_LIMITER_ROUNDS: {
-      if (value < 0 || value > 2) return TOMATIS_E_ARG;
-      if (p->lim_rounds == (int)value) return TOMATIS_OK;
-      p->lim_rounds = (int)value;
-      if (p->n_streams == 0 || p->lds) return TOMATIS_OK;
-      int rc = build_runs(p);
-      if (!rc) rc = limiter_accounting(p);
-      return rc;
-    }
     default: return TOMATIS_E_ARG;
   }
 }
@@ -3061,10 +2983,6 @@ int32_t tomatis_get_dev_option(int32_t key) {
   return tshared::g_dev[key];
 }
 
-int32_t tomatis_plan_limiter_rounds(tomatis_plan_t p) {
-  if (!p) return -1;
-  return (p->n1 > 0 && p->partner) ? 2 : 1;
-}
 
 int tomatis_apply_limiter(tomatis_plan_t p, float* y, const uint32_t* peaks, float limit, void* hs) {
   return limiter_launch(p, y, peaks, limit, 0, 0, hs);

@@ -57,16 +57,12 @@ struct MainArgs {
   uint32_t* err;        // TOMATIS_ERR_* bits
   int lim_spin;         // fused-limiter wait bound (polls of the chunk counter)
   unsigned long long* prof;  // TM_PROFILE builds only: per-phase wave cycles
-  // Two-round fused limiter (DESIGN.md §6 "Limiter rounds"): round 1 writes its
-  // output unscaled (defer_self: no rescale tail); in round 2 every run also
-  // scales the output of partner[run] (a round-1 run, -1: none): the hop blocks
-  // k_r2_plan listed (chunks complete after round 1 whose peak exceeds the
-  // limit) inside its frame loop, the rest in its tail.
-  int run_base;         // this launch runs [run_base, run_base + n_runs)
+  // Pipelined batches (tomatis_stft_ola_gated_pipelined / _pipelined): runs
+  // [run_base, run_base + n_runs); defer_self leaves this launch's output
+  // unscaled; per launched run 2 * (max_pieces + 1) words of k_r2_plan output:
+  // {count, first block left to the tail}, then count x {block, scale bits}
+  int run_base;
   int defer_self;
-  const int32_t* partner;   // round 2 only, indexed by run
-  // round 2: per launched run 2 * (max_pieces + 1) words: {count, first block
-  // left to the tail}, then count x {partner block, scale bits}
   const uint32_t* pieces;
   int max_pieces;
   // Pipelined batches (tomatis_stft_ola_gated_pipelined): the partner of every
@@ -86,8 +82,7 @@ struct MainArgs {
   const int32_t* gcarry;  // per run: state id before its first frame (< 0: unresolved)
   const float* gwin;      // per run: the 16 leaf sums of the frame before its first
 };
-void launch_r2_plan(const MainArgs& A, const uint32_t* chunk_final, uint32_t* pieces,
-                    hipStream_t s);
+void launch_r2_plan(const MainArgs& A, uint32_t* pieces, hipStream_t s);
 // k_gate_carry over every run of A (A.run_base = 0): carry-in state id and leaf
 // window per run; H_max frames of look-back before a run is left unresolved
 // gtf (optional): per-run transfer tables [n_runs][gate_D + 2] for chained

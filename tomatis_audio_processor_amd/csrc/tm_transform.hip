@@ -347,8 +347,9 @@ typedef __attribute__((address_space(4))) const uint32_t cu32;
 // GM: where the gain rows live (per-lane layout).  0: global (L2) only;
 // 1: all (<= 2) rows in LDS; 2: the two pure rows A.lds_row[0..1] in LDS, the
 // cross-fade lattice rows from global (row is wave-uniform, so is the branch).
-// PR: round 2 of the two-round fused limiter (MainArgs::partner): each interior
-// run also rescales its round-1 partner's output inside its frame loop.
+// PR: a pipelined batch (MainArgs::yprev): each interior run also applies the
+// limiter to its own slot of the previous batch's output inside its frame loop
+// (its "partner": the same run of the previous batch).
 // GT: in-kernel levels + gate (MainArgs::gated): each frame's r and state come
 // from the frame the kernel has loaded (no separate level pass, no row ids).
 template <int P, int NR, int SH, int CH, int GM, bool PF, bool NT, int WG, bool PR = false,
@@ -423,6 +424,19 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
 #endif
 
   const int seq = threadIdx.x / P, L = threadIdx.x % P;
+#if defined(TM_DEV_PRIO) || defined(TM_DEV_STAGGER)
+  {  // experiments: the second half of the block's waves (each SIMD's partner)
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (wv >= WG / 128) {
+#ifdef TM_DEV_PRIO
+      __builtin_amdgcn_s_setprio(1);
+#endif
+#ifdef TM_DEV_STAGGER
+      for (int i = 0; i < TM_DEV_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
+#endif
+    }
+  }
+#endif
   // wave-uniform run id (readfirstlane: run and stream descriptors load as scalars)
   const int run_loc = __builtin_amdgcn_readfirstlane(blockIdx.x * NSEQ + seq);
   const int run_id = A.run_base + run_loc;
@@ -653,9 +667,9 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       }
     };
     cf v[NR], nh[SH], o[SH];
-    // ---- round 2: rescale the partner's (round-1 run) blocks in this loop ----
+    // ---- pipelined: rescale the partner's (previous batch) blocks in this loop ----
     // k_r2_plan listed, for this run, the partner's hop blocks to scale (chunks
-    // round 1 completed whose peak exceeds the limit) with their scale, at most
+    // whose final peak exceeds the limit) with their scale, at most
     // one per frame: frame it loads piece it into this sequence's LDS slot by
     // LDS-DMA at its top and scales and stores it at its end (no VGPRs in
     // flight across the transform, which is at its register limit).
@@ -670,9 +684,8 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
     int np = 0;
     float* yP = ys;
     if constexpr (PR) {
-      // partner: a round-1 run of this launch, or (pipelined) this run's slot in
-      // the previous batch's output
-      const int pr = A.yprev ? run_id : __builtin_amdgcn_readfirstlane(A.partner[run_id]);
+      // partner: this run's slot in the previous batch's output
+      const int pr = run_id;
       plist = (cu32*)(A.pieces) + (int64_t)run_loc * 2 * (A.max_pieces + 1);
       np = (int)plist[0];
       if (np > 0) {
@@ -905,8 +918,8 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
     }
   }
   if constexpr (PR) {  // the partner's output not scaled in the frame loop
-    const bool prev = A.yprev != nullptr;  // previous batch: final, no waits
-    const int pr = valid ? (prev ? run_id : A.partner[run_id]) : -1;
+    const bool prev = true;  // the previous batch: final, no waits
+    const int pr = valid ? run_id : -1;
     if (pr >= 0 && done) {
       const Run RP = A.runs[pr];
       const TomatisStream SP = A.st[RP.s];
@@ -939,32 +952,25 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
 #endif
 }
 
-// Round 2 of the two-round fused limiter: for each run of the launch, the hop
-// blocks of its round-1 partner that its frame loop scales (one per frame):
-// blocks of chunks with no round-2 contributions (chunk_final) whose peak
-// exceeds the limit, in order, up to the first chunk that round 2 still
-// completes or the run's frame count.  Scale = limit / peak in float32, as the
-// limiter (src/process_tomatis.py:351-355).
-__global__ __launch_bounds__(64) void k_r2_plan(MainArgs A, const uint32_t* __restrict__ chunk_final,
-                                                uint32_t* __restrict__ out) {
+// Pipelined batches: for each run, the hop blocks of the same run of the
+// previous batch that its frame loop scales (one per frame): blocks of chunks
+// whose final peak exceeds the limit, in order, up to the run's frame count
+// (the rest go to its tail).  Scale = limit / peak in float32, as the limiter
+// (src/process_tomatis.py:351-355).
+__global__ __launch_bounds__(64) void k_r2_plan(MainArgs A, uint32_t* __restrict__ out) {
   // one wave per run; lanes take the partner's blocks 64 at a time
   const int t = blockIdx.x, lane = threadIdx.x;
   if (t >= A.n_runs) return;
   uint32_t* o = out + (int64_t)t * 2 * (A.max_pieces + 1);
   const int run = A.run_base + t;
-  const bool prev = A.yprev != nullptr;  // pipelined: the same run of the previous batch
-  const int pr = prev ? run : A.partner[run];
+  const int pr = run;  // the same run of the previous batch
   int n = 0, stop = 0;
   if (pr >= 0 && (A.runs[pr].last & kRunInterior) && (A.runs[run].last & kRunInterior)) {
     const Run R = A.runs[run], RP = A.runs[pr];
     const TomatisStream SP = A.st[RP.s];
     const int hop = A.hop;
     const int nit = (int)(R.kb - max<int64_t>(0, R.ka - (A.rmax - 1)));
-#ifdef TM_DEV_R2_TAIL_ONLY  // experiment: every partner block left to the tail
-    const int cap = 0;
-#else
     const int cap = min(nit, A.max_pieces);
-#endif
     const int nb = (int)(RP.kb - RP.ka);
     const int64_t s0 = SP.first_start + RP.ka * hop;
     stop = nb;
@@ -975,15 +981,14 @@ __global__ __launch_bounds__(64) void k_r2_plan(MainArgs A, const uint32_t* __re
       if (j < nb) {
         const int c = chunk_of(s0 + (int64_t)j * hop, SP);
         const int g = SP.chunk_base + c;
-        halt = (!prev && !chunk_final[g]) ||
-               ((A.edge_mask & 1) && c == 0) || ((A.edge_mask & 2) && c == SP.n_chunks - 1);
+        halt = ((A.edge_mask & 1) && c == 0) || ((A.edge_mask & 2) && c == SP.n_chunks - 1);
         if (!halt) {
-          const float peak = __uint_as_float((prev ? A.peaks_prev : A.peaks)[g]);
+          const float peak = __uint_as_float(A.peaks_prev[g]);
           want = peak > A.limit;
           sc = A.limit / peak;
         }
       }
-      // the walk ends at the first block of a chunk round 2 completes (or an edge chunk)
+      // the walk ends at the first block of an edge chunk (time shards)
       const uint64_t hb = __ballot(halt);
       const int first_halt = hb ? j0 + __builtin_ctzll(hb) : INT_MAX;
       want = want && j < first_halt;
@@ -1584,7 +1589,7 @@ void launch_main_pf(const MainArgs& A, int ch, hipStream_t s) {
   const dim3 g((A.n_runs + WG / P - 1) / (WG / P)), b(WG);
   if constexpr (P == 64 && (SH == 4 || SH == 8)) {
     if (A.gated) {  // in-kernel levels + gate (two-row tables: gm == 1, host-checked)
-      if (A.partner || A.yprev) {
+      if (A.yprev) {
         if constexpr (WG == 512 && SH <= 8) {
           if (ch == 2)
             hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 1, PF, NT, WG, true, true>), g, b, 0, s, A);
@@ -1600,7 +1605,7 @@ void launch_main_pf(const MainArgs& A, int ch, hipStream_t s) {
     }
   }
   if constexpr (P == 64 && WG == 512 && SH <= 8) {  // (LDS slots: host limits rounds to hop <= 512)
-    if (A.partner || A.yprev) {  // round 2 / pipelined batch (two-row tables: gm == 1)
+    if (A.yprev) {  // pipelined batch (LDS gain rows: gm 1, or gm 2 at hop 512)
       if constexpr (SH == 8) {
         // pipelined adaptive batches (cross-fade lattice: the pure rows in LDS)
         if (gm == 2) {
@@ -1650,14 +1655,14 @@ void launch_main(const MainArgs& A, int ch, int wg, hipStream_t s) {
 #endif
   if constexpr (P == 64) {
     // single-exchange FFT: 8.5 KB of exchange rows per sequence, so the tables
-    // are shared by 8 sequences (one 512-thread block per CU).  Otherwise round
-    // 2 of the two-round limiter takes 512-thread blocks (the per-sequence LDS
-    // slots of the partner rescale fit once per CU)
+    // are shared by 8 sequences (one 512-thread block per CU).  Otherwise a
+    // pipelined batch takes 512-thread blocks (the per-sequence LDS slots of
+    // the partner rescale fit once per CU)
     if constexpr (kFftX) {
       (void)wg;
       return launch_main_pf<P, NR, SH, false, true, 512>(A, ch, s);
     } else {
-      if (wg == 512 || A.partner || A.yprev) return launch_main_pf<P, NR, SH, false, true, 512>(A, ch, s);
+      if (wg == 512 || A.yprev) return launch_main_pf<P, NR, SH, false, true, 512>(A, ch, s);
       return launch_main_pf<P, NR, SH, false, true, 256>(A, ch, s);
     }
   }
@@ -1763,10 +1768,10 @@ void launch_lds_frames(const LdsArgs& A, hipStream_t s) {
 #undef LDS_M
 }
 
-void launch_r2_plan(const MainArgs& A, const uint32_t* chunk_final, uint32_t* pieces,
+void launch_r2_plan(const MainArgs& A, uint32_t* pieces,
                     hipStream_t s) {
   if (A.n_runs <= 0) return;
-  hipLaunchKernelGGL(k_r2_plan, dim3(A.n_runs), dim3(64), 0, s, A, chunk_final, pieces);
+  hipLaunchKernelGGL(k_r2_plan, dim3(A.n_runs), dim3(64), 0, s, A, pieces);
 }
 
 void launch_gate_carry(const MainArgs& A, int P, int SH, int ch, int32_t* gcarry, float* gwin,

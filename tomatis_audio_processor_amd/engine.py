@@ -28,7 +28,7 @@ import numpy as np
 
 from . import dsp
 from ._lib import (E_UNSUPPORTED, ERR_GATE_CARRY, ERR_LIMITER_WAIT, ERR_PAIR_BARRIER, F32, F64, NORM_EPS, NORM_MAX,
-                   OPT_FUSE_LIMITER, OPT_LIMITER_ROUNDS, OPT_LIMITER_SPIN, OPT_MINHOLD_SERIAL, TomatisPlanDesc, TomatisStream, check, lib,
+                   OPT_FUSE_LIMITER, OPT_LIMITER_SPIN, OPT_MINHOLD_SERIAL, TomatisPlanDesc, TomatisStream, check, lib,
                    ptr, stream_handle)
 
 PEAK_LIMIT = 0.999
@@ -139,16 +139,6 @@ class Plan:
     def option(self, option: int, default: int) -> int:
         """The value this wrapper last set for ``option`` (else ``default``)."""
         return self._opts.get(option, default)
-
-    def set_limiter_rounds(self, rounds: int):
-        """TOMATIS_OPT_LIMITER_ROUNDS: 0 auto, 1 one round, 2 two rounds (the
-        round-1 output is scaled inside round 2's frame loop)."""
-        self.set_option(OPT_LIMITER_ROUNDS, rounds)
-
-    @property
-    def limiter_rounds(self) -> int:
-        """2 when this plan's fused limiter runs in two rounds, else 1."""
-        return int(self.L.tomatis_plan_limiter_rounds(self.h))
 
     def set_limiter_spin(self, polls: int):
         """Fused-limiter wait bound (fault injection: 0 forces the recovery path)."""
