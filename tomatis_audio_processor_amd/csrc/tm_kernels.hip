@@ -1647,7 +1647,6 @@ struct tomatis_plan_s {
   float* gate_win = nullptr;
   int gate_cap = 0;
   uint16_t* gate_tf = nullptr;     // chained runs' transfer tables [gate_cap][D + 2]
-  int32_t* run_first = nullptr;    // per stream: first run index (n_streams + 1)
   // the look-back the carries in gate_carry belong to (input, run layout)
   const float* gl_x = nullptr;
   int gl_gen = -1;
@@ -1739,7 +1738,7 @@ int tomatis_plan_destroy(tomatis_plan_t p) {
                   p->aq, p->afin, p->acin,
                   p->chunk_need, p->chunk_done, p->chunk_rng, p->err, p->twL,
                   p->xs_pieces, p->gate_carry, p->gate_win,
-                  p->gate_tf, p->run_first,
+                  p->gate_tf,
                   p->pw_leaf, p->pw_prog, p->blue_b, p->blue_h, p->glb_work};
   for (void* q : ptrs) dfree(q);
   delete p;
@@ -1879,14 +1878,6 @@ static int build_runs(tomatis_plan_s* p) {
   if ((rc = dalloc_copy(&p->runs, runs))) return rc;
   p->hruns = runs;
   ++p->runs_gen;  // carries of an earlier look-back no longer match these runs
-  {  // first run of every stream (runs are in stream order)
-    std::vector<int32_t> rf(ns + 1, (int32_t)runs.size());
-    for (int i = (int)runs.size() - 1; i >= 0; --i) rf[runs[i].s] = i;
-    for (int st = ns - 1; st >= 0; --st) rf[st] = std::min(rf[st], rf[st + 1]);
-    dfree(p->run_first);
-    p->run_first = nullptr;
-    if ((rc = dalloc_copy(&p->run_first, rf))) return rc;
-  }
   return TOMATIS_OK;
 }
 
@@ -2600,7 +2591,7 @@ static int gate_lookback(tomatis_plan_s* p, const float* x, hipStream_t s) {
   A.ch = p->d.ch;
   A.gate_D = p->d.up_delay_frames;
   launch_gate_carry(A, p->P, p->SH, p->d.ch, p->gate_carry, p->gate_win,
-                    chain ? p->gate_tf : nullptr, p->run_first, p->n_streams, s);
+                    chain ? p->gate_tf : nullptr, s);
   return launch_check();
 }
 
@@ -2748,7 +2739,9 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
   }
   if (limit > 0.f) {
     if (!p->chunk_done) return TOMATIS_E_UNSUPPORTED;
-    if (hipMemsetAsync(p->chunk_done, 0, (size_t)p->total_chunks * 4, s)) return TOMATIS_E_HIP;
+    // flush counters of the in-launch limiter (a pipelined batch counts none)
+    if (!prev && hipMemsetAsync(p->chunk_done, 0, (size_t)p->total_chunks * 4, s))
+      return TOMATIS_E_HIP;
   }
   const int nseq = 256 / p->P;
   const int blocks = (p->n_runs + nseq - 1) / nseq;

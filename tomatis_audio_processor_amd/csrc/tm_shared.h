@@ -86,9 +86,9 @@ void launch_r2_plan(const MainArgs& A, uint32_t* pieces, hipStream_t s);
 // k_gate_carry over every run of A (A.run_base = 0): carry-in state id and leaf
 // window per run; H_max frames of look-back before a run is left unresolved
 // gtf (optional): per-run transfer tables [n_runs][gate_D + 2] for chained
-// runs, composed by k_gate_chain over run_first[stream .. stream + 1)
+// runs, composed by k_gate_chain (one thread per run)
 void launch_gate_carry(const MainArgs& A, int P, int SH, int ch, int32_t* gcarry, float* gwin,
-                       uint16_t* gtf, const int32_t* run_first, int n_streams, hipStream_t s);
+                       uint16_t* gtf, hipStream_t s);
 constexpr int kGateLookback = 512;       // look-back limit of a run that cannot chain
 constexpr int kGateLookbackMax = 4096;   // chained runs: frames back to the previous run's start
 constexpr int kGateChainStates = 1024;   // chaining needs gate_D + 2 <= this (transfer tables)

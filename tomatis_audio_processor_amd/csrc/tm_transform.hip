@@ -424,19 +424,6 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
 #endif
 
   const int seq = threadIdx.x / P, L = threadIdx.x % P;
-#if defined(TM_DEV_PRIO) || defined(TM_DEV_STAGGER)
-  {  // experiments: the second half of the block's waves (each SIMD's partner)
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (wv >= WG / 128) {
-#ifdef TM_DEV_PRIO
-      __builtin_amdgcn_s_setprio(1);
-#endif
-#ifdef TM_DEV_STAGGER
-      for (int i = 0; i < TM_DEV_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
-#endif
-    }
-  }
-#endif
   // wave-uniform run id (readfirstlane: run and stream descriptors load as scalars)
   const int run_loc = __builtin_amdgcn_readfirstlane(blockIdx.x * NSEQ + seq);
   const int run_id = A.run_base + run_loc;
@@ -509,7 +496,8 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   const int64_t s_ka = S.first_start + R.ka * HOP;
   int cid = chunk_of(s_ka, S);
   const int cid_first = cid;
-  uint32_t* const done = (A.limit > 0.f) ? A.chunk_done : nullptr;
+  // flush counters only for the in-launch limiter (a pipelined batch limits later)
+  uint32_t* const done = (A.limit > 0.f && !A.defer_self) ? A.chunk_done : nullptr;
   int64_t next_chunk_k = INT64_MAX;
   if (S.n_chunks > 1 && cid < S.n_chunks - 1)
     next_chunk_k = (S.chunk_first + (int64_t)cid * S.chunk_len - S.first_start) / HOP;
@@ -901,7 +889,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
     }
   }
   if (valid) flush_peak<P>(pk, cid, S, A.peaks, L, done);
-  if (valid && done && !A.defer_self) {
+  if (valid && done) {
     // this wave's own output range (stores of frames [ka, kb) and the stream tail)
     const int64_t s_last = S.first_start + (R.kb - 1) * HOP;
     const int64_t lo = max(s_ka, S.out_begin) - S.out_begin;
@@ -920,7 +908,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   if constexpr (PR) {  // the partner's output not scaled in the frame loop
     const bool prev = true;  // the previous batch: final, no waits
     const int pr = valid ? run_id : -1;
-    if (pr >= 0 && done) {
+    if (pr >= 0 && A.limit > 0.f) {
       const Run RP = A.runs[pr];
       const TomatisStream SP = A.st[RP.s];
       const int64_t s_kaP = SP.first_start + RP.ka * HOP;
@@ -1228,27 +1216,28 @@ __global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restri
   if (L == 0) carry[run] = id;
 }
 
-// Chained carries in run order, one lane per stream: a chained run's carry is
-// its transfer function applied to the previous run's carry (resolved, or
-// itself chained and composed just before); an unresolved predecessor leaves
-// it unresolved.
-__global__ __launch_bounds__(64) void k_gate_chain(const Run* __restrict__ runs, int n_runs,
-                                                   const int32_t* __restrict__ run_first,
-                                                   int n_streams, int nst,
-                                                   int32_t* __restrict__ carry,
-                                                   const uint16_t* __restrict__ tf) {
-  const int s = blockIdx.x * 64 + threadIdx.x;
-  if (s >= n_streams) return;
-  const int r1 = run_first[s + 1];
-  int prev = -1;
-  for (int r = run_first[s]; r < r1 && r < n_runs; ++r) {
-    int c = carry[r];
-    if (c == kGateChained) {
-      c = prev < 0 ? -1 : (int)tf[(int64_t)r * nst + prev];
-      carry[r] = c;
-    }
-    prev = c;
-  }
+// Chained carries, one thread per run: a chained run's carry is the transfer
+// functions of the chained runs from the nearest earlier non-chained run r0 up
+// to itself, applied in run order to carry[r0] (-1, unresolved, stays -1).  A
+// stream's first run never chains (kc = 0), so r0 is in the run's own stream.
+// Threads finish chained predecessors concurrently: a predecessor read as
+// already composed holds its final carry, which the walk may start from just
+// as well (relaxed 32-bit loads / stores).  Common case (no chained runs): one
+// coalesced load per run.
+__global__ __launch_bounds__(256) void k_gate_chain(int n_runs, int nst,
+                                                    int32_t* __restrict__ carry,
+                                                    const uint16_t* __restrict__ tf) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= n_runs) return;
+  if (__hip_atomic_load(carry + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != kGateChained)
+    return;
+  int r0 = r - 1, c = -1;
+  while (r0 >= 0 && (c = __hip_atomic_load(carry + r0, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT)) == kGateChained)
+    --r0;
+  if (r0 < 0) c = -1;
+  for (int q = r0 + 1; q <= r && c >= 0; ++q) c = (int)tf[(int64_t)q * nst + c];
+  __hip_atomic_store(carry + r, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Generic hop: same transform, windowed frame outputs to scratch, then a gather.
@@ -1775,7 +1764,7 @@ void launch_r2_plan(const MainArgs& A, uint32_t* pieces,
 }
 
 void launch_gate_carry(const MainArgs& A, int P, int SH, int ch, int32_t* gcarry, float* gwin,
-                       uint16_t* gtf, const int32_t* run_first, int n_streams, hipStream_t s) {
+                       uint16_t* gtf, hipStream_t s) {
   if (A.n_runs <= 0 || P != 64) return;
   const dim3 g(A.n_runs), b(64);
   if (SH == 8) {
@@ -1787,9 +1776,9 @@ void launch_gate_carry(const MainArgs& A, int P, int SH, int ch, int32_t* gcarry
   } else {
     return;
   }
-  if (gtf && run_first && n_streams > 0)
-    hipLaunchKernelGGL(k_gate_chain, dim3((n_streams + 63) / 64), dim3(64), 0, s, A.runs, A.n_runs,
-                       run_first, n_streams, A.gate_D + 2, gcarry, gtf);
+  if (gtf)
+    hipLaunchKernelGGL(k_gate_chain, dim3((A.n_runs + 255) / 256), dim3(256), 0, s, A.n_runs,
+                       A.gate_D + 2, gcarry, gtf);
 }
 
 void launch_lds_gather(const LdsArgs& A, hipStream_t s) {

@@ -9,7 +9,7 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('s
 tail -1 $D/smoke.log
 timeout -k 10 600 python -u bench.py > $D/bench.log 2>&1 || { tail -20 $D/bench.log; exit 1; }
 tail -1 $D/bench.log | cut -c1-400
-for w in c3 c4 c5x c5 c2ts; do
+for w in c3 c4 c4h c5x c5 c2ts; do
   timeout -k 10 300 python -u bench.py --workload $w --steps 10 --warmup 3 --cpu-sample-s 0 > $D/bench_$w.log 2>&1 || { tail -20 $D/bench_$w.log; exit 1; }
   echo "$w $(grep -o '"ms_per_step": [0-9.]*' $D/bench_$w.log) $(grep -o '"kernel_ms": [0-9.]*' $D/bench_$w.log) $(grep -o '"frac": [0-9.]*' $D/bench_$w.log | head -1)"
 done
