@@ -74,26 +74,53 @@ class ChainC5:
     on the stage-1 output, all device-resident.  The residual curve is a fixed
     synthetic diff spectrum (+-4 dB ripple), smoothed and clamped by the
     reference's own rules (dsp.smooth_on_logfreq / build_eq_from_residual).
-    ``marks`` time the stage-1 transform (the dominant launch)."""
+    ``marks`` time the stage-1 transform (the dominant launch).
 
-    def __init__(self, engine, ss, sr, n_fft, hop):
+    ``pipelined``: stage 1 is a batch pipeline (pass k's transform limits pass
+    k-1's output), so stage 2 of pass k-1 runs after stage 1 of pass k, on
+    that pass's (alternating) output buffer; flush() limits the last stage-1
+    output and runs its stage 2.  K steps + flush = K passes of both stages."""
+
+    def __init__(self, engine, ss, sr, n_fft, hop, pipelined=True):
         from tomatis_audio_processor_amd import dsp
         self.s1 = engine.GatePipeline(ss, gate_ui=50, gate_offset=-90, n_fft=n_fft, hop=hop,
-                                      xfade_ms=500.0)
+                                      xfade_ms=500.0, pipelined=pipelined)
         res = self.s1.result()
-        ss2 = engine.StreamSet(x=self.s1.y, offs=res.out_offs, lens=res.out_lens, ch=ss.ch, sr=sr)
         rf = np.geomspace(20.0, sr / 2, 400)
         rd = 4.0 * np.sin(np.log2(rf / 20.0) * 1.7) * np.exp(-rf / 12000.0)
         res_s = dsp.smooth_on_logfreq(rf, rd, win=41)
         lin, _ = dsp.build_eq_from_residual(np.fft.rfftfreq(n_fft, 1.0 / sr), rf, res_s)
-        self.s2 = engine.StaticEqPipeline(ss2, lin, n_fft=n_fft, hop=hop, pad=False)
+        bufs = self.s1._ys if self.s1.pipelined else [self.s1.y]
+        self.s2 = {}
+        for y in bufs:  # one stage-2 pipeline per stage-1 output buffer
+            ss2 = engine.StreamSet(x=y, offs=res.out_offs, lens=res.out_lens, ch=ss.ch, sr=sr)
+            self.s2[y.data_ptr()] = engine.StaticEqPipeline(ss2, lin, n_fft=n_fft, hop=hop,
+                                                            pad=False)
+        self.pending2 = None  # stage-1 buffer whose stage 2 waits for its limiter
+
+    @property
+    def pipelined(self):
+        return self.s1.pipelined
 
     def run(self, marks=None, check_device=True):
+        prev = self.s1.y if self.s1.pending else None
         self.s1.run(marks=marks, check_device=check_device)
-        return self.s2.run(check_device=check_device)
+        if not self.s1.pending:  # unpipelined: stage 2 on this pass at once
+            return self.s2[self.s1.y.data_ptr()].run(check_device=check_device)
+        if prev is not None:     # pass k-1's output is final now
+            self.s2[prev.data_ptr()].run(check_device=check_device)
+        return None
+
+    def flush(self):
+        """the last pass: stage 1's limiter, then its stage 2 (that result)"""
+        if self.s1.pending:
+            y = self.s1.y
+            self.s1.flush()
+            return self.s2[y.data_ptr()].run(check_device=False)
+        return None
 
     def finish(self):
-        return self.s1.finish() | self.s2.finish()
+        return self.s1.finish() | max(p.finish() for p in self.s2.values())
 
     def result(self):
         return self.s1.result()
@@ -102,7 +129,7 @@ class ChainC5:
 def plans_of(pipe):
     """Every tomatis plan a bench pipeline launches on."""
     if isinstance(pipe, ChainC5):
-        return [pipe.s1.plan, pipe.s2.plan]
+        return [pipe.s1.plan] + [p.plan for p in pipe.s2.values()]
     if hasattr(pipe, "pipes"):          # AdaptiveGroups
         return [p.plan for p in pipe.pipes]
     if hasattr(pipe, "rn"):             # timeshard.RankStep
@@ -335,8 +362,10 @@ def main():
         pipe = engine.GatePipeline(ss, gate_ui=50, n_fft=n_fft, hop=hop,
                                    pipelined=not a.no_pipeline)
     elif mode == "xfade":
+        # batch pipeline (two-pass chain, n_fft 4096: the partner blocks through
+        # VGPRs); the timed region ends with flush()
         pipe = engine.GatePipeline(ss, gate_ui=50, gate_offset=-90, n_fft=n_fft, hop=hop,
-                                   xfade_ms=500.0)
+                                   xfade_ms=500.0, pipelined=not a.no_pipeline)
     elif mode == "adaptive":
         # two stream groups: one group's host phase overlaps the other's device work
         # (batch pipeline as in standard mode: the global limiter of pass k in
@@ -344,12 +373,14 @@ def main():
         pipe = engine.AdaptiveGroups(ss, groups=int(os.environ.get("TOMATIS_C3_GROUPS", "2")),
                                      n_fft=n_fft, hop=hop, pipelined=not a.no_pipeline)
     elif mode == "chain":
-        pipe = ChainC5(engine, ss, sr, n_fft, hop)
+        pipe = ChainC5(engine, ss, sr, n_fft, hop, pipelined=not a.no_pipeline)
         stages = 2
     torch.cuda.synchronize()
 
     for _ in range(a.warmup):
         pipe.run()          # device error word checked after every warm-up pass
+    if hasattr(pipe, "flush"):
+        pipe.flush()        # pipelined: the timed region starts with nothing pending
     torch.cuda.synchronize()
     if ws > 1:
         dist.barrier()

@@ -277,7 +277,8 @@ int tomatis_stft_ola_gated_after_lookback(tomatis_plan_t plan, const float* x,
  * so the rescale's HBM traffic overlaps the transform instead of being a tail.
  * The last batch's output is limited by tomatis_apply_limiter(plan, y,
  * chunk_peak_bits, limit).  Results are bit-identical to the unpipelined call.
- * y, chunk_peak_bits must not alias prev_y, prev_peak_bits.
+ * y, chunk_peak_bits must not alias prev_y, prev_peak_bits.  The call zeroes
+ * chunk_peak_bits itself (inside the launch sequence; the caller need not).
  * TOMATIS_E_UNSUPPORTED where tomatis_stft_ola_gated is, or without limiter
  * chunks (the caller runs the unpipelined call). */
 int tomatis_stft_ola_gated_pipelined(tomatis_plan_t plan, const float* x,
@@ -290,7 +291,8 @@ int tomatis_stft_ola_gated_pipelined(tomatis_plan_t plan, const float* x,
  * :298-345, whose global limiter is one chunk per stream): as
  * tomatis_stft_ola_limited except that y is left unscaled and prev_y (the
  * previous call's output with this plan, peaks prev_peak_bits) is limited
- * inside this launch.  TOMATIS_E_UNSUPPORTED unless n_fft 2048, hop <= 512
+ * inside this launch; chunk_peak_bits zeroed by the call as above.
+ * TOMATIS_E_UNSUPPORTED unless n_fft 2048, hop <= 512
  * (hop 512 for cross-fade row tables) and limiter chunks exist. */
 int tomatis_stft_ola_pipelined(tomatis_plan_t plan, const float* x, const float* gain_rows,
                                int32_t n_rows, const uint16_t* rows, float* y,

@@ -152,14 +152,60 @@ def test_pipelined_gate_fallback():
 
 
 def test_pipelined_declines():
-    """hop 1024 (no fused gate) and xfade run unpipelined, results at once."""
+    """hop > 1024 at n_fft 4096, hop 1024 at 2048 (no partner-rescale
+    instantiation) run unpipelined, results at once."""
     torch, E = _engine()
     sr, n = 44100, 44100 * 20
     ss = E.StreamSet.synthetic(1, n, 2, sr, seed0=5)
-    for kw in (dict(n_fft=2048, hop=1024), dict(n_fft=2048, hop=512, xfade_ms=500.0)):
+    for kw in (dict(n_fft=2048, hop=1024), dict(n_fft=4096, hop=2048),
+               dict(n_fft=4096, hop=2048, xfade_ms=500.0)):
         pipe = E.GatePipeline(ss, gate_ui=50, pipelined=True, **kw)
         res = pipe.run()
-        assert res is not None and not pipe.pending, kw
+        assert res is not None and not pipe.pending and not pipe.pipelined, kw
+
+
+@pytest.mark.parametrize("case", [
+    # (name, streams, seconds, ch, sr, n_fft, hop, xfade_ms, per-stream gains)
+    ("xfade_2048", 3, 40, 2, 44100, 2048, 512, 500.0, [1.0, 0.2, 0.6]),
+    ("xfade_4096_c5x", 2, 60, 2, 96000, 4096, 1024, 500.0, [1.0, 0.3]),
+    ("std_4096", 3, 40, 2, 48000, 4096, 1024, None, [1.0, 0.05, 0.5]),
+    ("xfade_4096_mono_hop512", 2, 30, 1, 44100, 4096, 512, 250.0, [1.0, 0.4]),
+])
+def test_pipelined_two_pass(case):
+    """The two-pass chain (levels, gate, xfade alpha from tomatis_gate_std) with
+    pipelined transforms (tomatis_stft_ola_pipelined): n_fft 2048 with the
+    cross-fade's pure rows in LDS, n_fft 4096 with the partner blocks through
+    VGPRs (two-wave frames).  Every pass's output, chunk peaks, r, states and
+    alpha equal an unpipelined pass bit for bit."""
+    torch, E = _engine()
+    _, ns, secs, ch, sr, n_fft, hop, xf, gains = case
+    n = sr * secs + 391
+    xs = _inputs(E, torch, ns, n, ch, sr, gains, 3)
+    ss = E.StreamSet.synthetic(ns, n, ch, sr, seed0=1)
+    kw = dict(gate_ui=50, n_fft=n_fft, hop=hop, xfade_ms=xf, gate_offset=-90)
+    ref = E.GatePipeline(ss, **kw)
+    refs = []
+    for x in xs:
+        ss.x.copy_(x)
+        ref.run()
+        al = ref.alpha.clone() if ref.alpha is not None else None
+        refs.append((ref.y.clone(), ref.peaks.clone(), ref.r.clone(), ref.states.clone(), al))
+    del ref
+    pipe = E.GatePipeline(ss, pipelined=True, **kw)
+    F = pipe.plan.total_frames
+    held = None
+    for k, x in enumerate(xs):
+        ss.x.copy_(x)
+        assert pipe.run() is None and pipe.pending and pipe.pipelined, "pipelined pass"
+        if held is not None:
+            _check(torch, F, (held[0].clone(), held[1].clone(), held[2], held[3]), refs[k - 1][:4], k - 1)
+            if held[4] is not None:
+                assert torch.equal(held[4][:F], refs[k - 1][4][:F]), f"pass {k - 1}: alpha differs"
+        al = pipe.alpha.clone() if pipe.alpha is not None else None
+        held = (pipe.y, pipe.peaks, pipe.r.clone(), pipe.states.clone(), al)
+    res = pipe.result()
+    assert not pipe.pending
+    _check(torch, F, (res.y, res.chunk_peaks, held[2], held[3]), refs[-1][:4], len(xs) - 1)
 
 
 @pytest.mark.parametrize("groups", [1, 2])

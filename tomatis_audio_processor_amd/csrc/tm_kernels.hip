@@ -35,6 +35,10 @@ using namespace tgate;
 namespace {
 
 constexpr int kSeg = 1024;           // gate segment length (frames)
+// xfade alpha segment length (frames): each segment's alpha recurrence is one
+// lane's latency chain (k_alpha_sync / k_alpha_prefix), so short segments, many
+// waves (C5x: 3.5 k segments of 128 frames instead of 440 of 1024)
+constexpr int kASeg = 128;
 constexpr int kLevelLds = 12288;     // floats of LDS for the levels span
 constexpr int kMaxGateStates = 65535;  // uint16 state ids (transfer tables)
 
@@ -622,8 +626,8 @@ __global__ __launch_bounds__(64) void k_alpha_sync(const TomatisStream* __restri
                                                    double* __restrict__ alpha,
                                                    int32_t* __restrict__ seg_q,
                                                    double* __restrict__ seg_final) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_st[kSeg];
-  __shared__ double s_a[kSeg];
+  __shared__ __attribute__((aligned(16))) uint8_t s_st[kASeg];
+  __shared__ double s_a[kASeg];
   __shared__ int s_q;
   const int i = blockIdx.x;
   if (i >= nseg) return;
@@ -741,8 +745,8 @@ __global__ __launch_bounds__(64) void k_alpha_prefix(const TomatisStream* __rest
                                                      const double* __restrict__ carry_in,
                                                      uint16_t* __restrict__ rows,
                                                      double* __restrict__ alpha) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_st[kSeg];
-  __shared__ double s_a[kSeg];
+  __shared__ __attribute__((aligned(16))) uint8_t s_st[kASeg];
+  __shared__ double s_a[kASeg];
   const int i = blockIdx.x;
   if (i >= nseg) return;
   const int q = seg_q[i];
@@ -1446,9 +1450,23 @@ __global__ __launch_bounds__(256) void k_limiter(float* __restrict__ y,
   const float sc = limit / peak;
   const int64_t n = (C.p1 - C.p0) * ch;
   float* base = y + S.out_off + C.p0 * ch;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x)
-    base[i] = base[i] * sc;
+  // 16-byte accesses: scalar head to alignment, float4 body, scalar tail
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t head = std::min<int64_t>(n, (int64_t)((16 - ((uintptr_t)base & 15)) & 15) >> 2);
+  const int64_t nb = (n - head) >> 2;
+  if (tid < head) base[tid] = base[tid] * sc;
+  float4* __restrict__ b4 = reinterpret_cast<float4*>(base + head);
+  for (int64_t i = tid; i < nb; i += stride) {
+    float4 v = b4[i];
+    v.x = v.x * sc;
+    v.y = v.y * sc;
+    v.z = v.z * sc;
+    v.w = v.w * sc;
+    b4[i] = v;
+  }
+  const int64_t t0 = head + 4 * nb;
+  if (tid < n - t0) base[t0 + tid] = base[t0 + tid] * sc;
 }
 
 __device__ __forceinline__ void absmax_body(const float* __restrict__ x, int64_t n,
@@ -1599,6 +1617,10 @@ struct tomatis_plan_s {
   int n_segs = 0;
   int32_t* seg_first = nullptr;
   int32_t* seg_count = nullptr;
+  GateSeg* asegs = nullptr;        // xfade alpha segments (kASeg frames)
+  int n_asegs = 0;
+  int32_t* aseg_first = nullptr;
+  int32_t* aseg_count = nullptr;
   uint16_t* tf = nullptr;
   uint16_t* seg_start = nullptr;
   float* win = nullptr;
@@ -1732,6 +1754,7 @@ const char* tomatis_status_string(int s) {
 int tomatis_plan_destroy(tomatis_plan_t p) {
   if (!p) return TOMATIS_OK;
   void* ptrs[] = {p->st, p->runs, p->lblocks, p->segs, p->seg_first, p->seg_count, p->tf,
+                  p->asegs, p->aseg_first, p->aseg_count,
                   p->seg_start, p->win, p->winS, p->win2, p->winv, p->twN, p->twP, p->scratch,
                   p->pos_base, p->chunks, p->mh_tf, p->mh_cnt, p->mh_off, p->mh_sym, p->mh_soff, p->mh_bs, p->mh_pc, p->mh_gtf, p->mh_gcnt, p->mh_goff, p->mh_arr, p->gperm,
                   p->grp_base, p->leaf_base, p->leaves, p->gsum, p->gcarry, p->gcarry_in,
@@ -2003,18 +2026,29 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
   {
     std::vector<GateSeg> sg;
     std::vector<int32_t> first(ns), count(ns);
-    for (int s = 0; s < ns; ++s) {
-      const int64_t F = p->hs[s].n_frames;
-      first[s] = (int32_t)sg.size();
-      for (int64_t a = 0; a < F; a += kSeg) {
-        GateSeg g;
-        g.s = s;
-        g.k0 = a;
-        g.nf = (int)std::min<int64_t>(kSeg, F - a);
-        sg.push_back(g);
+    auto segment = [&](int len) {
+      sg.clear();
+      for (int s = 0; s < ns; ++s) {
+        const int64_t F = p->hs[s].n_frames;
+        first[s] = (int32_t)sg.size();
+        for (int64_t a = 0; a < F; a += len) {
+          GateSeg g;
+          g.s = s;
+          g.k0 = a;
+          g.nf = (int)std::min<int64_t>(len, F - a);
+          sg.push_back(g);
+        }
+        count[s] = (int32_t)sg.size() - first[s];
       }
-      count[s] = (int32_t)sg.size() - first[s];
+    };
+    if (d.alpha_mode == 1) {
+      segment(kASeg);
+      p->n_asegs = (int)sg.size();
+      if ((rc = dalloc_copy(&p->asegs, sg))) return rc;
+      if ((rc = dalloc_copy(&p->aseg_first, first))) return rc;
+      if ((rc = dalloc_copy(&p->aseg_count, count))) return rc;
     }
+    segment(kSeg);
     p->n_segs = (int)sg.size();
     if ((rc = dalloc_copy(&p->segs, sg))) return rc;
     p->gate_excl = dev_opt(TOMATIS_DEV_GATE_TF, 0) == 0;
@@ -2421,19 +2455,21 @@ int tomatis_gate_std(tomatis_plan_t p, const float* r, uint8_t* states, uint16_t
                          p->n_streams, states, nxf, rows, alpha_out);
       return launch_check();
     }
+    if (p->n_asegs == 0) return launch_check();
     if (!p->aq) {
-      if (hipMalloc(reinterpret_cast<void**>(&p->aq), (size_t)p->n_segs * sizeof(int32_t)) ||
-          hipMalloc(reinterpret_cast<void**>(&p->afin), (size_t)p->n_segs * sizeof(double)) ||
-          hipMalloc(reinterpret_cast<void**>(&p->acin), (size_t)p->n_segs * sizeof(double)))
+      const size_t na = (size_t)p->n_asegs;
+      if (hipMalloc(reinterpret_cast<void**>(&p->aq), na * sizeof(int32_t)) ||
+          hipMalloc(reinterpret_cast<void**>(&p->afin), na * sizeof(double)) ||
+          hipMalloc(reinterpret_cast<void**>(&p->acin), na * sizeof(double)))
         return TOMATIS_E_NOMEM;
     }
-    const unsigned gs = (unsigned)p->n_segs;  // one wave per segment
-    hipLaunchKernelGGL(k_alpha_sync, dim3(gs), dim3(64), 0, s, p->st, p->segs, p->n_segs, states,
+    const unsigned gs = (unsigned)p->n_asegs;  // one wave per alpha segment
+    hipLaunchKernelGGL(k_alpha_sync, dim3(gs), dim3(64), 0, s, p->st, p->asegs, p->n_asegs, states,
                        nxf, rows, alpha_out, p->aq, p->afin);
     hipLaunchKernelGGL(k_alpha_chain, dim3((p->n_streams + 63) / 64), dim3(64), 0, s, p->st,
-                       p->n_streams, p->segs, p->seg_first, p->seg_count, states, nxf, p->aq,
+                       p->n_streams, p->asegs, p->aseg_first, p->aseg_count, states, nxf, p->aq,
                        p->afin, p->acin);
-    hipLaunchKernelGGL(k_alpha_prefix, dim3(gs), dim3(64), 0, s, p->st, p->segs, p->n_segs,
+    hipLaunchKernelGGL(k_alpha_prefix, dim3(gs), dim3(64), 0, s, p->st, p->asegs, p->n_asegs,
                        states, nxf, p->aq, p->acin, rows, alpha_out);
   }
   return launch_check();
@@ -2665,7 +2701,6 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
       return TOMATIS_E_NOMEM;
     p->gperm_rows = n_rows;
   }
-  launch_gain_perm(p->P, p->NR, p->fx, gains, n_rows, N / 2 + 1, p->gperm, s);
   MainArgs A;
   A.x = x;
   A.y = y;
@@ -2702,6 +2737,13 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
       A.lds_row[0] = 2;
       A.lds_row[1] = n_rows - 1;
     }
+  }
+  {  // every row in LDS (gm 1): the kernel prologue permutes the caller's rows
+    const bool in_lds = !p->generic && !(p->P == 128 && p->NR == 32) && A.n_rows_lds == n_rows &&
+                        !A.lds_mixed;
+    A.graw = in_lds ? gains : nullptr;
+    A.g_nb = N / 2 + 1;
+    if (!in_lds) launch_gain_perm(p->P, p->NR, p->fx, gains, n_rows, N / 2 + 1, p->gperm, s);
   }
   A.limit = limit;
   A.chunk_done = p->chunk_done;
@@ -2767,8 +2809,10 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
       A.peaks_prev = prev->peaks;
       A.pieces = p->xs_pieces;
       A.max_pieces = p->xs_max_pieces;
-      launch_r2_plan(A, p->xs_pieces, s);
+      launch_r2_plan(A, p->xs_pieces, p->total_chunks, p->P, s);  // (zeroes this launch's peaks)
       if ((rc = launch_check())) return rc;
+    } else if (hipMemsetAsync(peaks, 0, (size_t)p->total_chunks * 4, s)) {
+      return TOMATIS_E_HIP;
     }
     launch_transform(A, p->P, p->NR, p->SH, ch, transform_wg(p->P, p->NR), s);
     return launch_check();
@@ -2817,7 +2861,8 @@ static int limiter_launch(tomatis_plan_t p, float* y, const uint32_t* peaks, flo
   if (!p || !y || !peaks) return TOMATIS_E_ARG;
   if (p->n_chunkdesc == 0) return TOMATIS_OK;
   const int64_t per = p->max_chunk * p->d.ch;
-  const unsigned gx = (unsigned)std::min<int64_t>(std::max<int64_t>(1, (per + 1023) / 1024), 4096);
+  // ~2 float4 per thread per chunk
+  const unsigned gx = (unsigned)std::min<int64_t>(std::max<int64_t>(1, (per + 2047) / 2048), 4096);
   hipLaunchKernelGGL(k_limiter, dim3(gx, p->n_chunkdesc), dim3(256), 0, (hipStream_t)hs, y, p->st,
                      p->chunks, peaks, limit, p->d.ch, sel, edge_mask);
   return launch_check();
@@ -2915,11 +2960,14 @@ int tomatis_stft_ola_pipelined(tomatis_plan_t p, const float* x, const float* ga
     return TOMATIS_E_ARG;
   // the partner-rescale instantiations: n_fft 2048 interior loop, hop <= 512,
   // gain rows in LDS (one or two rows; the cross-fade lattice's pure rows at
-  // hop 512), per-chunk accounting
+  // hop 512); n_fft 4096 (two-wave frames, gain rows in L2, partner blocks
+  // through VGPRs), hop <= 1024 at the 512-thread launch; per-chunk accounting
   const TomatisPlanDesc& d = p->d;
   const bool lds_rows = n_rows <= 2 ||
                         (d.alpha_mode != 0 && p->SH == 8 && dev_opt(TOMATIS_DEV_GAIN_LDS, 1) != 0);
-  if (p->generic || p->lds || p->P != 64 || p->NR != 32 || p->SH > 8 || !lds_rows ||
+  const bool p64 = p->P == 64 && lds_rows;
+  const bool p128 = p->P == 128 && transform_wg(p->P, p->NR) == 512;
+  if (p->generic || p->lds || p->NR != 32 || p->SH > 8 || !(p64 || p128) ||
       p->total_chunks <= 0 || !p->chunk_need)
     return TOMATIS_E_UNSUPPORTED;
   const PrevBatch pb{prev_y, prev_peaks};

@@ -71,6 +71,11 @@ struct MainArgs {
   // kernel's own output stays unscaled (defer_self) for the next batch.
   float* yprev;
   const uint32_t* peaks_prev;
+  // gain rows as the caller passed them ([rows][n_bins], not permuted): when
+  // set, the LDS-gain prologue (all rows in LDS) permutes them itself and the
+  // host launches no k_gain_perm
+  const float* graw;
+  int g_nb;
   // in-kernel levels + gate (tomatis_stft_ola_gated, DESIGN.md §5 "Fused
   // levels"): every frame's r (numpy pairwise order) and gate state are computed
   // from the input the transform loads and written here; each run starts from
@@ -82,7 +87,8 @@ struct MainArgs {
   const int32_t* gcarry;  // per run: state id before its first frame (< 0: unresolved)
   const float* gwin;      // per run: the 16 leaf sums of the frame before its first
 };
-void launch_r2_plan(const MainArgs& A, uint32_t* pieces, hipStream_t s);
+// (also zeroes A.peaks[0, n_zero): this pipelined launch's chunk peaks)
+void launch_r2_plan(const MainArgs& A, uint32_t* pieces, int n_zero, int P, hipStream_t s);
 // k_gate_carry over every run of A (A.run_base = 0): carry-in state id and leaf
 // window per run; H_max frames of look-back before a run is left unresolved
 // gtf (optional): per-run transfer tables [n_runs][gate_D + 2] for chained

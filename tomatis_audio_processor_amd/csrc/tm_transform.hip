@@ -352,6 +352,20 @@ typedef __attribute__((address_space(4))) const uint32_t cu32;
 // (its "partner": the same run of the previous batch).
 // GT: in-kernel levels + gate (MainArgs::gated): each frame's r and state come
 // from the frame the kernel has loaded (no separate level pass, no row ids).
+// gain entry t of the per-lane layout ([rows][N], entry e = lq(i, L) of a row)
+// from rows [rows][n_bins]: the bin the forward FFT leaves in register i of lane
+// L (mirrored: the gain is real and even), x 1/N (exact) x that register's
+// output scale (FX: the single-exchange FFT's layout, fftx_bin)
+template <int P, int NR, bool FX>
+__device__ __forceinline__ float gain_perm_at(const float* __restrict__ g, int n_bins, int t) {
+  constexpr int N = NR * P;
+  const int row = t / N, e = t - row * N;
+  const int q = e >> 2, L = q % P, i = (q / P) * 4 + (e & 3);
+  int b = !FX ? fft_bin<P, NR>(L, i) : (P == 64 ? fftx_bin(L, i) : fftx128_bin(L, i));
+  b = (b <= N / 2) ? b : N - b;
+  return (g[(int64_t)row * n_bins + b] * (1.0f / (float)N)) * (FX ? sig_at<32>(i) : sig_at<8>(i & 7));
+}
+
 template <int P, int NR, int SH, int CH, int GM, bool PF, bool NT, int WG, bool PR = false,
           bool GT = false>
 __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(MainArgs A) {
@@ -381,8 +395,9 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   __shared__ __attribute__((aligned(16))) float s_winv[SHQ * P];  // lane-quad layout
   __shared__ __attribute__((aligned(16))) cf s_buf[NSEQ][SEQ_CF];
   __shared__ __attribute__((aligned(16))) float s_gain[GM ? 2 * N : 4];
-  // PR: one hop block per sequence for the partner rescale (LDS-DMA target)
-  __shared__ __attribute__((aligned(16))) char s_pbuf[PR ? NSEQ * SH * P * CH * 4 : 16];
+  // PR: one hop block per sequence for the partner rescale (LDS-DMA target;
+  // n_fft 4096 has no LDS left and takes the blocks through VGPRs)
+  __shared__ __attribute__((aligned(16))) char s_pbuf[PR && P == 64 ? NSEQ * SH * P * CH * 4 : 16];
   for (int i = threadIdx.x; i < NR * P; i += WG) s_twN[i] = A.twN[i];
   if constexpr (LT) {  // [m/2][l][m&1] = W_P^{(l%8)*m}
     for (int i = threadIdx.x; i < 8 * P; i += WG) {
@@ -408,7 +423,11 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   }
   if constexpr (GM == 1) {
     const int nr = A.n_rows_lds;
-    for (int i = threadIdx.x; i < nr * N; i += WG) s_gain[i] = A.gains[i];
+    if (A.graw) {
+      for (int i = threadIdx.x; i < nr * N; i += WG) s_gain[i] = gain_perm_at<P, NR, FX>(A.graw, A.g_nb, i);
+    } else {
+      for (int i = threadIdx.x; i < nr * N; i += WG) s_gain[i] = A.gains[i];
+    }
   } else if constexpr (GM == 2) {
     for (int i = threadIdx.x; i < 2 * N; i += WG)
       s_gain[i] = A.gains[(int64_t)A.lds_row[i >= N] * N + (i >= N ? i - N : i)];
@@ -602,7 +621,31 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
 
   bool fast_run = false;
   if constexpr (P == 64) fast_run = valid && (R.last & kRunInterior);
-  int p_done = 0;  // PR: partner blocks [0, p_done) handled in the frame loop
+  int p_done = 0;  // PR: partner blocks [p_lead, p_done) handled in the frame loop
+  int p_lead = 0;   // (leading partial output blocks of a stream's first run: tail)
+  // PR: k_r2_plan's list of this run's partner blocks (previous batch's output)
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  constexpr int HOPB = HOP * CH * 4;
+  cu32* plist = nullptr;
+  int np = 0;
+  float* yP = ys;
+  if constexpr (PR) {
+    if (valid) {
+      // partner: this run's slot in the previous batch's output
+      const int pr = run_id;
+      plist = (cu32*)(A.pieces) + (int64_t)run_loc * 2 * (A.max_pieces + 1);
+      np = (int)plist[0];
+      if (np > 0) {
+        const Run RP = A.runs[pr];
+        const TomatisStream SP = A.st[RP.s];
+        const int64_t off = SP.out_off + CH * (SP.first_start + RP.ka * HOP - SP.out_begin);
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)off);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)off >> 32));
+        yP = (A.yprev ? A.yprev : A.y) + (int64_t)(((uint64_t)hi << 32) | lo);
+      }
+    }
+  }
+  constexpr bool PL = PR && P == 64;  // the partner's blocks by LDS-DMA (fast loop)
   if (fast_run) {
     // Interior run (host-marked): every frame of [kfirst, kb) reads a full frame
     // and every emitted hop block is a full interior block (no stream edges, no
@@ -661,30 +704,11 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
     // one per frame: frame it loads piece it into this sequence's LDS slot by
     // LDS-DMA at its top and scales and stores it at its end (no VGPRs in
     // flight across the transform, which is at its register limit).
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    constexpr int HOPB = HOP * CH * 4;
-    constexpr int BQ = PR ? HOPB / 1024 : 1;  // b128 per lane per block
-    static_assert(!PR || HOPB % 1024 == 0, "a hop block is whole b128 per lane");
+    constexpr int BQ = PL ? HOPB / 1024 : 1;  // b128 per lane per block
+    static_assert(!PL || HOPB % 1024 == 0, "a hop block is whole b128 per lane");
     // (wave-uniform values made explicit: a VGPR resource or LDS address here
     // becomes a waterfall loop)
-    char* const pslot = s_pbuf + (PR ? __builtin_amdgcn_readfirstlane(seq * HOPB) : 0);
-    cu32* plist = nullptr;
-    int np = 0;
-    float* yP = ys;
-    if constexpr (PR) {
-      // partner: this run's slot in the previous batch's output
-      const int pr = run_id;
-      plist = (cu32*)(A.pieces) + (int64_t)run_loc * 2 * (A.max_pieces + 1);
-      np = (int)plist[0];
-      if (np > 0) {
-        const Run RP = A.runs[pr];
-        const TomatisStream SP = A.st[RP.s];
-        const int64_t off = SP.out_off + CH * (SP.first_start + RP.ka * HOP - SP.out_begin);
-        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)off);
-        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)off >> 32));
-        yP = (A.yprev ? A.yprev : A.y) + (int64_t)(((uint64_t)hi << 32) | lo);
-      }
-    }
+    char* const pslot = s_pbuf + (PL ? __builtin_amdgcn_readfirstlane(seq * HOPB) : 0);
     uint32_t rw_nx = GT ? 0u : row_word(0);  // (GT: no row ids)
     {  // frame 0, null stores (the loop's issue pattern), new hop of frame 1
       ld_old(0, v);
@@ -706,7 +730,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
         row = row_of(rw_nx, it);
         rw_nx = row_word(min(it + 1, nit - 1));
       }
-      if constexpr (PR) {
+      if constexpr (PL) {
         // piece it of the partner -> LDS slot (branch-free: past the list the
         // resource is empty, the load returns zeros and the store drops)
         const int blk = (int)plist[2 + 2 * min(it, np)];
@@ -756,7 +780,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       for (int j = 0; j < SH; ++j) v[NO + j] = cf{opaque_f(nh[j].x), opaque_f(nh[j].y)};
       store_out(o, emit ? ry : rnull, emit ? (it - nwarm) * (HOP * CH * 4) : 0);
       ld_new(min(it + 2, nit - 1), nh);
-      if constexpr (PR) {
+      if constexpr (PL) {
         // piece it: scale, store (its LDS-DMA is counted by vmcnt only)
         // behind this frame's critical loads: only ld_old / store_out / ld_new
         // (NO + 2 SH instructions) were issued after the LDS-DMA, so this count
@@ -785,7 +809,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       }
       TPROF(6, acc[0].x);
     }
-    if constexpr (PR) p_done = (int)plist[1];  // first block the frame loop left
+    if constexpr (PL) p_done = (int)(plist[1] & 0xffffffu);  // first block the loop left
 #ifdef TM_PROFILE
     if (L == 0) {
       for (int i = 0; i < 7; ++i) atomicAdd(A.prof + i, tacc[i]);
@@ -825,6 +849,15 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
     cf nx[NR];
     uint32_t row_nx = GT ? 0u : load_row(kfirst);  // (GT: no row ids)
     if constexpr (PF) load_frame(kfirst, nx);
+    // PR (n_fft 4096: no LDS left for the LDS-DMA slots): piece it of the
+    // partner through VGPRs, loaded right after frame it's input, scaled and
+    // stored after its transform -- before the frame's own stores, so the wait
+    // for it waits for nothing issued later; past the list the resource is
+    // empty (zero loads, dropped stores).  Streaming (nt) accesses: the pieces
+    // must not evict the frames' overlap from L2
+    constexpr bool PV = PR && P > 64;
+    constexpr int PQ = PV ? HOPB / (16 * P) : 1;  // b128 per lane per block
+    static_assert(!PV || HOPB % (16 * P) == 0, "a hop block is whole b128 per lane");
 
     for (int it = 0; it < nit; ++it) {
       const int64_t k = kfirst + it;
@@ -843,8 +876,36 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       } else {
         load_frame(k, v);
       }
+      // (the piece's loads after the frame's: the in-order wait for the frame's
+      // input does not wait for them)
+      f32x4 pbk[PQ];
+      __amdgpu_buffer_rsrc_t rpp;
+      float psc = 1.f;
+      if constexpr (PV) {
+        const int blk = (int)plist[2 + 2 * min(it, np)];
+        psc = __uint_as_float(plist[3 + 2 * min(it, np)]);
+        rpp = mk_rsrc(yP + (int64_t)blk * (HOP * CH), it < np ? (uint32_t)HOPB : 0u);
+  #pragma unroll
+        for (int u = 0; u < PQ; ++u)
+          pbk[u] = __builtin_amdgcn_raw_buffer_load_b128(rpp, L * 16, u * 16 * P, 2);  // (nt)
+      }
       if constexpr (GT) row = gate_frame(v, k, live && k >= R.ka);
       transform(v, row);
+      if constexpr (PV) {
+  #pragma unroll
+        for (int u = 0; u < PQ; ++u) {
+          const f4v t = f4v{__uint_as_float(pbk[u].x), __uint_as_float(pbk[u].y),
+                            __uint_as_float(pbk[u].z), __uint_as_float(pbk[u].w)} * psc;
+          const f32x4 b = {__float_as_uint(t.x), __float_as_uint(t.y), __float_as_uint(t.z),
+                           __float_as_uint(t.w)};
+          __builtin_amdgcn_raw_buffer_store_b128(b, rpp, L * 16, u * 16 * P, 2);  // (nt)
+          // one wait state before any VALU write of the store's data VGPRs
+          // (tools/store_hazard.py)
+          __builtin_amdgcn_sched_barrier(0);
+          __asm__ volatile("s_nop 0");
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
       if (live && k >= R.ka) {
         if (k == next_chunk_k) {
           flush_peak<P>(pk, cid, S, A.peaks, L, done);
@@ -887,6 +948,10 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   #pragma unroll
       for (int i = 0; i < NC; ++i) acc[i] = v[i + SH];
     }
+    if constexpr (PV) {
+      p_done = valid ? (int)(plist[1] & 0xffffffu) : 0;
+      p_lead = valid ? (int)(plist[1] >> 24) : 0;
+    }
   }
   if (valid) flush_peak<P>(pk, cid, S, A.peaks, L, done);
   if (valid && done) {
@@ -914,9 +979,8 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       const int64_t s_kaP = SP.first_start + RP.ka * HOP;
       const int64_t s_lastP = SP.first_start + (RP.kb - 1) * HOP;
       const int64_t endP = SP.out_begin + SP.out_len;
-      const int64_t lo = max(s_kaP + (int64_t)p_done * HOP, SP.out_begin) - SP.out_begin;
-      const int64_t hi = min(s_lastP + ((RP.last & 1) ? (int64_t)N : (int64_t)HOP), endP) - SP.out_begin;
-      if (lo < hi) {
+      auto tail = [&](int64_t lo, int64_t hi) {  // output-relative [lo, hi)
+        if (lo >= hi) return;
         const int nw = P / 64, w = L >> 6;
         const int64_t span = hi - lo, per = (span + nw - 1) / nw;
         const int64_t wlo = lo + per * w, whi = min(hi, wlo + per);
@@ -925,7 +989,12 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
           if (((A.edge_mask & 1) && c == 0) || ((A.edge_mask & 2) && c == SP.n_chunks - 1)) continue;
           limit_own<CH>(A, SP, SP.chunk_base + c, wlo, whi, L & 63, prev);
         }
-      }
+      };
+      const int64_t hi = min(s_lastP + ((RP.last & 1) ? (int64_t)N : (int64_t)HOP), endP) - SP.out_begin;
+      if (p_lead > 0)  // the leading partial blocks
+        tail(max(s_kaP, SP.out_begin) - SP.out_begin,
+             min(s_kaP + (int64_t)p_lead * HOP - SP.out_begin, hi));
+      tail(max(s_kaP + (int64_t)max(p_done, p_lead) * HOP, SP.out_begin) - SP.out_begin, hi);
     }
   }
 #ifdef TM_PROFILE
@@ -944,16 +1013,21 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
 // previous batch that its frame loop scales (one per frame): blocks of chunks
 // whose final peak exceeds the limit, in order, up to the run's frame count
 // (the rest go to its tail).  Scale = limit / peak in float32, as the limiter
-// (src/process_tomatis.py:351-355).
-__global__ __launch_bounds__(64) void k_r2_plan(MainArgs A, uint32_t* __restrict__ out) {
+// (src/process_tomatis.py:351-355).  any_run: the transform scales pieces in
+// its generic loop too (n_fft 4096), so any run takes them, up to the partner's
+// first block that is not a full output block; otherwise (n_fft 2048: the
+// interior loop only) both runs must be interior.
+__global__ __launch_bounds__(64) void k_r2_plan(MainArgs A, uint32_t* __restrict__ out,
+                                                int n_zero, int any_run) {
   // one wave per run; lanes take the partner's blocks 64 at a time
   const int t = blockIdx.x, lane = threadIdx.x;
+  for (int i = t * 64 + lane; i < n_zero; i += gridDim.x * 64) A.peaks[i] = 0u;
   if (t >= A.n_runs) return;
   uint32_t* o = out + (int64_t)t * 2 * (A.max_pieces + 1);
   const int run = A.run_base + t;
   const int pr = run;  // the same run of the previous batch
-  int n = 0, stop = 0;
-  if (pr >= 0 && (A.runs[pr].last & kRunInterior) && (A.runs[run].last & kRunInterior)) {
+  int n = 0, stop = 0, lead = 0;
+  if (pr >= 0 && (any_run || ((A.runs[pr].last & kRunInterior) && (A.runs[run].last & kRunInterior)))) {
     const Run R = A.runs[run], RP = A.runs[pr];
     const TomatisStream SP = A.st[RP.s];
     const int hop = A.hop;
@@ -961,22 +1035,28 @@ __global__ __launch_bounds__(64) void k_r2_plan(MainArgs A, uint32_t* __restrict
     const int cap = min(nit, A.max_pieces);
     const int nb = (int)(RP.kb - RP.ka);
     const int64_t s0 = SP.first_start + RP.ka * hop;
+    // leading blocks that start before the output (a stream's first run):
+    // skipped here, scaled by the tail
+    lead = (int)min<int64_t>(min(nb, 255), max<int64_t>(0, (SP.out_begin - s0 + hop - 1) / hop));
     stop = nb;
     for (int j0 = 0; j0 < nb && j0 < stop; j0 += 64) {
       const int j = j0 + lane;
       bool want = false, halt = false;
       float sc = 1.f;
       if (j < nb) {
-        const int c = chunk_of(s0 + (int64_t)j * hop, SP);
+        const int64_t sj = s0 + (int64_t)j * hop;
+        const int c = chunk_of(sj, SP);
         const int g = SP.chunk_base + c;
-        halt = ((A.edge_mask & 1) && c == 0) || ((A.edge_mask & 2) && c == SP.n_chunks - 1);
-        if (!halt) {
+        halt = ((A.edge_mask & 1) && c == 0) || ((A.edge_mask & 2) && c == SP.n_chunks - 1) ||
+               (j >= lead && (sj < SP.out_begin || sj + hop > SP.out_begin + SP.out_len));
+        if (!halt && j >= lead) {
           const float peak = __uint_as_float(A.peaks_prev[g]);
           want = peak > A.limit;
           sc = A.limit / peak;
         }
       }
-      // the walk ends at the first block of an edge chunk (time shards)
+      // the walk ends at the first block of an edge chunk (time shards) or the
+      // first partial output block
       const uint64_t hb = __ballot(halt);
       const int first_halt = hb ? j0 + __builtin_ctzll(hb) : INT_MAX;
       want = want && j < first_halt;
@@ -1000,9 +1080,9 @@ __global__ __launch_bounds__(64) void k_r2_plan(MainArgs A, uint32_t* __restrict
       if (first_halt != INT_MAX) stop = min(stop, first_halt);
     }
   }
-  if (lane == 0) {
+  if (lane == 0) {  // (stop < 2^24: runs are at most 2^20 frames; lead < 256)
     o[0] = (uint32_t)n;
-    o[1] = (uint32_t)stop;
+    o[1] = (uint32_t)stop | ((uint32_t)lead << 24);
   }
 }
 
@@ -1313,12 +1393,7 @@ __global__ void k_gain_perm(const float* __restrict__ g, int n_rows, int n_bins,
   constexpr int N = NR * P;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_rows * N) return;
-  const int row = t / N, e = t - row * N;  // e = lq(i, L)
-  const int q = e >> 2, L = q % P, i = (q / P) * 4 + (e & 3);
-  int b = !FX ? fft_bin<P, NR>(L, i) : (P == 64 ? fftx_bin(L, i) : fftx128_bin(L, i));
-  b = (b <= N / 2) ? b : N - b;
-  // x the forward FFT's output scale of register i (its last DFT's output)
-  out[t] = (g[(int64_t)row * n_bins + b] * (1.0f / (float)N)) * (FX ? sig_at<32>(i) : sig_at<8>(i & 7));
+  out[t] = gain_perm_at<P, NR, FX>(g, n_bins, t);
 }
 
 // generic-hop OLA gather: one thread per output position (frame order preserved)
@@ -1608,6 +1683,13 @@ void launch_main_pf(const MainArgs& A, int ch, hipStream_t s) {
       return;
     }
   }
+  if constexpr (P == 128 && NR == 32 && WG == 512 && SH <= 8) {
+    if (A.yprev) {  // pipelined batch, n_fft 4096 (gain rows in L2; partner blocks in VGPRs)
+      if (ch == 2) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 0, PF, NT, WG, true>), g, b, 0, s, A);
+      else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, 0, PF, NT, WG, true>), g, b, 0, s, A);
+      return;
+    }
+  }
 #ifdef TM_DEV_ONE_KERNEL  // dev/asm studies: one instantiation (stereo, LDS gains)
   (void)gm;
   (void)ch;
@@ -1757,10 +1839,12 @@ void launch_lds_frames(const LdsArgs& A, hipStream_t s) {
 #undef LDS_M
 }
 
-void launch_r2_plan(const MainArgs& A, uint32_t* pieces,
-                    hipStream_t s) {
-  if (A.n_runs <= 0) return;
-  hipLaunchKernelGGL(k_r2_plan, dim3(A.n_runs), dim3(64), 0, s, A, pieces);
+void launch_r2_plan(const MainArgs& A, uint32_t* pieces, int n_zero, int P, hipStream_t s) {
+  if (A.n_runs <= 0) {
+    if (n_zero > 0) (void)hipMemsetAsync(A.peaks, 0, (size_t)n_zero * 4, s);
+    return;
+  }
+  hipLaunchKernelGGL(k_r2_plan, dim3(A.n_runs), dim3(64), 0, s, A, pieces, n_zero, P > 64 ? 1 : 0);
 }
 
 void launch_gate_carry(const MainArgs& A, int P, int SH, int ch, int32_t* gcarry, float* gwin,

@@ -395,12 +395,13 @@ class GatePipeline:
         the transform kernel (tomatis_stft_ola_gated) where the library takes
         the shape; False, or a shape it declines, runs the two-pass chain.
         ``pipelined``: successive run() calls form a batch pipeline
-        (tomatis_stft_ola_gated_pipelined): each pass leaves its output
+        (tomatis_stft_ola_gated_pipelined; the two-pass chain -- xfade, n_fft
+        4096 -- through tomatis_stft_ola_pipelined): each pass leaves its output
         unscaled and limits the PREVIOUS pass's output inside its own transform
         (two output buffers, alternating), so the limiter's HBM re-read overlaps
         compute instead of ending every pass.  A pass's output is final after
         the next run() or flush(); result() flushes.  Same results bit for bit.
-        Shapes the pipelined call declines run unpipelined."""
+        Shapes the pipelined calls decline run unpipelined."""
         torch = _torch()
         _check_fft(n_fft, hop, ss.ch)
         self.ss, self.n_fft, self.hop = ss, n_fft, hop
@@ -479,7 +480,7 @@ class GatePipeline:
         self.fused_levels = bool(fused_levels) and not self.xfade
         self.gated_used = False   # the last run() took tomatis_stft_ola_gated
         self.gate_fallbacks = 0   # gated passes re-run on the two-pass chain
-        self.pipelined = bool(pipelined) and self.fused_levels
+        self.pipelined = bool(pipelined)
         self.pending = False      # pipelined: self.y awaits its limiter
         if self.pipelined:
             self._ys = [self.y, torch.empty_like(self.y)]
@@ -507,7 +508,7 @@ class GatePipeline:
         self._two_pass(marks)
         if check_device:
             self.finish()
-        return self.result()
+        return None if self.pending else self.result()
 
     def _gated(self, marks=None) -> bool:
         """levels + gate + transform + limiter in one pass over the input (the
@@ -538,8 +539,7 @@ class GatePipeline:
         nxt = 1 - self._cur
         prev_y = self._ys[self._cur] if self.pending else None
         prev_pk = self._pks[self._cur] if self.pending else None
-        self._pks[nxt].zero_()
-        if marks:
+        if marks:  # (the call zeroes this pass's chunk peaks itself)
             marks[0].record()
         rc = L.tomatis_stft_ola_gated_pipelined(
             self.plan.h, ptr(self.ss.x), ptr(self.gains), self.n_rows, ptr(self._ys[nxt]),
@@ -562,18 +562,39 @@ class GatePipeline:
                                               PEAK_LIMIT, stream_handle()), "apply_limiter")
             self.pending = False
 
-    def _two_pass(self, marks=None):
+    def _two_pass(self, marks=None, pipelined=True):
         L, P, hs = lib(), self.plan.h, stream_handle()
         check(L.tomatis_levels(P, ptr(self.ss.x), ptr(self.r), F32, hs), "levels")
         check(L.tomatis_gate_std(P, ptr(self.r), ptr(self.states), ptr(self.rows),
                                  ptr(self.alpha), hs), "gate_std")
         if marks:
             marks[0].record()
-        self._transform()
+        if not (pipelined and self.pipelined and self._rows_pipelined_pass()):
+            self.flush()
+            self._limited()
         if marks:
             marks[1].record()
 
-    def _transform(self):
+    def _rows_pipelined_pass(self) -> bool:
+        """The two-pass chain's transform as a pipelined pass (gain-row ids from
+        tomatis_gate_std); False (nothing launched) when the library declines."""
+        nxt = 1 - self._cur
+        prev_y = self._ys[self._cur] if self.pending else None
+        prev_pk = self._pks[self._cur] if self.pending else None
+        rc = lib().tomatis_stft_ola_pipelined(  # (zeroes this pass's chunk peaks)
+            self.plan.h, ptr(self.ss.x), ptr(self.gains), self.n_rows, ptr(self.rows),
+            ptr(self._ys[nxt]), ptr(self._pks[nxt]), PEAK_LIMIT, ptr(prev_y), ptr(prev_pk),
+            stream_handle())
+        if rc == E_UNSUPPORTED:
+            self.pipelined = False
+            return False
+        check(rc, "stft_ola_pipelined")
+        self._cur = nxt
+        self.y, self.peaks = self._ys[nxt], self._pks[nxt]
+        self.pending = True
+        return True
+
+    def _limited(self):
         """transform + OLA + per-chunk limiter (fused in-kernel when chunks are short)"""
         self.peaks.zero_()
         check(lib().tomatis_stft_ola_limited(self.plan.h, ptr(self.ss.x), ptr(self.gains),
@@ -591,11 +612,15 @@ class GatePipeline:
                 self.gated_used = False
                 self.gate_fallbacks += 1
                 self.pending = False
-                self._two_pass()
+                self._two_pass(pipelined=False)
             # a limiter-wait redo of the gated pass: the transform alone cannot
             # recompute states, so the two-pass chain runs with the unfused limiter
             return finish_plan(self.plan, redo_gate, "GatePipeline", redo_gate=redo_gate)
-        return finish_plan(self.plan, self._transform, "GatePipeline")
+
+        def redo():  # (unpipelined, into the same buffer)
+            self.pending = False
+            self._limited()
+        return finish_plan(self.plan, redo, "GatePipeline")
 
     def result(self) -> Result:
         self.flush()
@@ -737,8 +762,7 @@ class AdaptivePipeline:
         nxt = 1 - self._cur
         prev_y = self._ys[self._cur] if self.pending else None
         prev_pk = self._pks[self._cur] if self.pending else None
-        self._pks[nxt].zero_()
-        rc = lib().tomatis_stft_ola_pipelined(
+        rc = lib().tomatis_stft_ola_pipelined(  # (zeroes this pass's chunk peaks)
             self.plan.h, ptr(self.ss.x), ptr(self.gains), self.n_rows, ptr(self.rows),
             ptr(self._ys[nxt]), ptr(self._pks[nxt]), PEAK_LIMIT, ptr(prev_y), ptr(prev_pk),
             stream_handle())
