@@ -112,3 +112,37 @@ def test_xfade_alpha_parallel_matches_sequential(n_fft, hop, sr, xfade_ms):
     for i in range(len(xs)):
         assert a_par[i].tobytes() == a_seq[i].tobytes()
         assert y_par[i].tobytes() == y_seq[i].tobytes()
+
+
+def test_xfade_alpha_unsynced_segments():
+    """States that flip faster than the cross-fade can settle (every 0.2 s
+    against xf + 2 = 49 frames) leave whole alpha segments without a sync
+    frame: k_alpha_chain walks them from their carry-in, in segment order.
+    Equal to the sequential float64 recurrence bit for bit."""
+    torch, E = _engine()
+    sr, n_fft, hop = 48000, 2048, 512
+    rng = np.random.default_rng(5)
+    xs = []
+    for n in (sr * 60 + 123, sr * 25 + 7):
+        t = np.arange(n)
+        env = np.where((t // int(0.2 * sr)) % 2 == 0, 10 ** (-20 / 20), 10 ** (-60 / 20))
+        env[2 * n // 3:] = 10 ** (-20 / 20)  # then steady: segments sync again
+        xs.append((rng.standard_normal((n, 2)) * env[:, None] * 0.5).astype(np.float32))
+
+    def run(env):
+        with _dev(env):
+            ss = E.StreamSet.from_arrays(xs, sr)
+            pipe = E.GatePipeline(ss, gate_ui=50, gate_offset=-90, n_fft=n_fft, hop=hop,
+                                  xfade_ms=500.0, up_delay_ms=10.0)
+            res = pipe.run()
+            torch.cuda.synchronize()
+            return ([res.stream_alpha(i) for i in range(len(xs))],
+                    [res.stream_states(i) for i in range(len(xs))])
+
+    a_seq, s_seq = run({"TOMATIS_ALPHA_SEQ": 1})
+    a_par, s_par = run({})
+    flips = int(np.count_nonzero(np.diff(s_seq[0].astype(np.int8))))
+    assert flips > 100, flips  # the states do flip faster than the fade settles
+    for i in range(len(xs)):
+        assert np.array_equal(s_par[i], s_seq[i])
+        assert a_par[i].tobytes() == a_seq[i].tobytes()

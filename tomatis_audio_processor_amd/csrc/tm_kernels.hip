@@ -710,29 +710,49 @@ __global__ __launch_bounds__(64) void k_alpha_sync(const TomatisStream* __restri
   }
 }
 
-// pass 2: one thread per stream: carry-in alpha of every segment
-__global__ void k_alpha_chain(const TomatisStream* __restrict__ st, int n_streams,
-                              const GateSeg* __restrict__ segs, const int32_t* __restrict__ seg_first,
-                              const int32_t* __restrict__ seg_count,
-                              const uint8_t* __restrict__ states, int xf,
-                              const int32_t* __restrict__ seg_q,
-                              const double* __restrict__ seg_final, double* __restrict__ carry_in) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+// pass 2: one wave per stream: carry-in alpha of every segment.  Lanes take 64
+// segments at a time; a segment with a sync frame hands its final alpha on
+// directly, one without is walked from its carry-in in segment order (lane by
+// lane, wave-uniform)
+__global__ __launch_bounds__(64) void k_alpha_chain(const TomatisStream* __restrict__ st,
+                                                    int n_streams,
+                                                    const GateSeg* __restrict__ segs,
+                                                    const int32_t* __restrict__ seg_first,
+                                                    const int32_t* __restrict__ seg_count,
+                                                    const uint8_t* __restrict__ states, int xf,
+                                                    const int32_t* __restrict__ seg_q,
+                                                    const double* __restrict__ seg_final,
+                                                    double* __restrict__ carry_in) {
+  const int s = blockIdx.x;
   if (s >= n_streams) return;
+  const int lane = threadIdx.x;
   const TomatisStream S = st[s];
   const double step = xf > 0 ? 1.0 / xf : 1.0;
-  double c = 0.0;
-  for (int i = seg_first[s], e = seg_first[s] + seg_count[s]; i < e; ++i) {
-    carry_in[i] = c;
-    const GateSeg G = segs[i];
-    if (seg_q[i] < G.nf) {
-      c = seg_final[i];
-    } else {  // no sync frame: the whole segment from the carry
-      for (int j = 0; j < G.nf; ++j) {
-        const double tgt = states[S.frame_base + G.k0 + j] == 1 ? 0.0 : 1.0;
-        c = (xf > 0) ? alpha_step(c, tgt, step) : tgt;
+  double c = 0.0;  // alpha before the chunk's first segment (wave-uniform)
+  const int first = seg_first[s], end = seg_first[s] + seg_count[s];
+  for (int base = first; base < end; base += 64) {
+    const int i = base + lane;
+    const bool valid = i < end;
+    const GateSeg G = valid ? segs[i] : GateSeg{0, 1, 0};
+    const bool synced = valid && seg_q[i] < G.nf;
+    double after = synced ? seg_final[i] : 0.0;  // alpha after segment i
+    uint64_t um = __ballot(valid && !synced);
+    while (um) {  // unsynced segments in order: walk each from its carry-in
+      const int u = __builtin_ctzll(um);
+      um &= um - 1;
+      const double prev = __shfl(after, u > 0 ? u - 1 : 0);
+      double a = u > 0 ? prev : c;
+      const GateSeg Gu = segs[base + u];
+      for (int j = 0; j < Gu.nf; ++j) {
+        const double tgt = states[S.frame_base + Gu.k0 + j] == 1 ? 0.0 : 1.0;
+        a = (xf > 0) ? alpha_step(a, tgt, step) : tgt;
       }
+      if (lane == u) after = a;
     }
+    const double up = __shfl_up(after, 1);
+    if (valid) carry_in[i] = lane == 0 ? c : up;
+    const int last = min(63, end - 1 - base);
+    c = __shfl(after, last);
   }
 }
 
@@ -2466,7 +2486,7 @@ int tomatis_gate_std(tomatis_plan_t p, const float* r, uint8_t* states, uint16_t
     const unsigned gs = (unsigned)p->n_asegs;  // one wave per alpha segment
     hipLaunchKernelGGL(k_alpha_sync, dim3(gs), dim3(64), 0, s, p->st, p->asegs, p->n_asegs, states,
                        nxf, rows, alpha_out, p->aq, p->afin);
-    hipLaunchKernelGGL(k_alpha_chain, dim3((p->n_streams + 63) / 64), dim3(64), 0, s, p->st,
+    hipLaunchKernelGGL(k_alpha_chain, dim3(p->n_streams), dim3(64), 0, s, p->st,
                        p->n_streams, p->asegs, p->aseg_first, p->aseg_count, states, nxf, p->aq,
                        p->afin, p->acin);
     hipLaunchKernelGGL(k_alpha_prefix, dim3(gs), dim3(64), 0, s, p->st, p->asegs, p->n_asegs,
