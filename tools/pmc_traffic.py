@@ -2,6 +2,7 @@
 """Write profiles/pmc_traffic.json from rocprofv3 FETCH_SIZE / WRITE_SIZE passes.
 
 Usage: tools/pmc_traffic.py PMC_DIR WORKLOAD [--kernel k_stft_ola] [--alg-bytes B]
+                            [--base BASE_DIR [--base-kernel K]]
 
 PMC_DIR holds the per-pass rocprofv3 outputs of tools/pmc.sh or
 tools/pmc_fetch.sh (p*/run_counter_collection.csv).  For the fused kernel the
@@ -12,6 +13,12 @@ bytes of a wide coalesced streaming read, so reads = 2 x FETCH_SIZE.  The
 kernel's input loads are 8-byte-per-lane buffer loads, a width the guide lists
 as uncalibrated, so the uncorrected figure is kept beside the corrected one.
 bench.py reads "hbm_bytes_per_launch" for its roofline.traffic field.
+
+--base: a pipelined launch reads its own input (8-B lanes) and the previous
+batch's limited blocks (16-B lanes, the partner rescale).  BASE_DIR is the
+same kernel's run with no chunk over the limit (bench --input-gain 0.05): its
+FETCH_SIZE is the input part, taken as reported; the excess over it is the
+partner part, corrected x2 (the guide's factor for 16-B streaming reads).
 """
 import csv
 import glob
@@ -40,6 +47,22 @@ def main():
     fetch_kib = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"])
     write_kib = sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"])
     rd = (2.0 if reads == "x2" else 1.0) * fetch_kib * 1024.0
+    base_kib = None
+    if "--base" in a:
+        bv = []
+        # (--base-kernel: the base is another instantiation, e.g. the same
+        # run's first, unpipelined pass)
+        bk = a[a.index("--base-kernel") + 1] if "--base-kernel" in a else kern
+        for f in sorted(glob.glob(os.path.join(a[a.index("--base") + 1], "p*",
+                                               "run_counter_collection.csv"))):
+            for r in csv.DictReader(open(f)):
+                if bk in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE":
+                    bv.append(float(r["Counter_Value"]))
+        if not bv:
+            sys.exit(f"no FETCH_SIZE dispatches of {kern} under the base run")
+        base_kib = sum(bv) / len(bv)
+        rd = (base_kib + 2.0 * max(0.0, fetch_kib - base_kib)) * 1024.0
+        reads = "base+2x"
     wr = write_kib * 1024.0
     out_path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                             "profiles", "pmc_traffic.json")
@@ -59,7 +82,12 @@ def main():
                           "limiter-inactive run (bench --input-gain 0.05), where FETCH_SIZE is "
                           "1.08x the input bytes (each input byte once + warm-up halos)"
                           if reads == "raw" else
+                          "reads = FETCH_SIZE of the no-limit run (input, 8-B lanes, as "
+                          "reported) + 2 x the excess (the partner rescale's 16-B reads)"
+                          if reads == "base+2x" else
                           "reads = 2 x FETCH_SIZE (gfx950, 16-B/lane streaming-read factor)")}
+    if base_kib is not None:
+        rec["base_fetch_size_kib"] = base_kib
     if alg:
         rec["alg_bytes_per_launch"] = alg
         rec["traffic_over_alg"] = (rd + wr) / alg
