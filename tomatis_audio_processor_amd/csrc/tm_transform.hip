@@ -41,6 +41,20 @@ namespace {
 #else
 #define TPROF(i, dep)
 #endif
+// gain entry t of the per-lane layout ([rows][N], entry e = lq(i, L) of a row)
+// from rows [rows][n_bins]: the bin the forward FFT leaves in register i of lane
+// L (mirrored: the gain is real and even), x 1/N (exact) x that register's
+// output scale (FX: the single-exchange FFT's layout, fftx_bin)
+template <int P, int NR, bool FX>
+__device__ __forceinline__ float gain_perm_at(const float* __restrict__ g, int n_bins, int t) {
+  constexpr int N = NR * P;
+  const int row = t / N, e = t - row * N;
+  const int q = e >> 2, L = q % P, i = (q / P) * 4 + (e & 3);
+  int b = !FX ? fft_bin<P, NR>(L, i) : (P == 64 ? fftx_bin(L, i) : fftx128_bin(L, i));
+  b = (b <= N / 2) ? b : N - b;
+  return (g[(int64_t)row * n_bins + b] * (1.0f / (float)N)) * (FX ? sig_at<32>(i) : sig_at<8>(i & 7));
+}
+
 // ===========================================================================
 // Fused STFT -> gain -> ISTFT -> OLA -> normalise (register OLA, hop % P == 0)
 // ===========================================================================
@@ -347,25 +361,12 @@ typedef __attribute__((address_space(4))) const uint32_t cu32;
 // GM: where the gain rows live (per-lane layout).  0: global (L2) only;
 // 1: all (<= 2) rows in LDS; 2: the two pure rows A.lds_row[0..1] in LDS, the
 // cross-fade lattice rows from global (row is wave-uniform, so is the branch).
-// PR: a pipelined batch (MainArgs::yprev): each interior run also applies the
-// limiter to its own slot of the previous batch's output inside its frame loop
-// (its "partner": the same run of the previous batch).
+// PR: a pipelined batch (MainArgs::yprev): each run also applies the limiter
+// to its own slot of the previous batch's output inside its frame loop (its
+// "partner": the same run of the previous batch) -- by LDS-DMA in the n_fft
+// 2048 interior loop, through VGPRs in the generic loop (n_fft 4096).
 // GT: in-kernel levels + gate (MainArgs::gated): each frame's r and state come
 // from the frame the kernel has loaded (no separate level pass, no row ids).
-// gain entry t of the per-lane layout ([rows][N], entry e = lq(i, L) of a row)
-// from rows [rows][n_bins]: the bin the forward FFT leaves in register i of lane
-// L (mirrored: the gain is real and even), x 1/N (exact) x that register's
-// output scale (FX: the single-exchange FFT's layout, fftx_bin)
-template <int P, int NR, bool FX>
-__device__ __forceinline__ float gain_perm_at(const float* __restrict__ g, int n_bins, int t) {
-  constexpr int N = NR * P;
-  const int row = t / N, e = t - row * N;
-  const int q = e >> 2, L = q % P, i = (q / P) * 4 + (e & 3);
-  int b = !FX ? fft_bin<P, NR>(L, i) : (P == 64 ? fftx_bin(L, i) : fftx128_bin(L, i));
-  b = (b <= N / 2) ? b : N - b;
-  return (g[(int64_t)row * n_bins + b] * (1.0f / (float)N)) * (FX ? sig_at<32>(i) : sig_at<8>(i & 7));
-}
-
 template <int P, int NR, int SH, int CH, int GM, bool PF, bool NT, int WG, bool PR = false,
           bool GT = false>
 __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(MainArgs A) {
@@ -1668,7 +1669,7 @@ void launch_main_pf(const MainArgs& A, int ch, hipStream_t s) {
       return;
     }
   }
-  if constexpr (P == 64 && WG == 512 && SH <= 8) {  // (LDS slots: host limits rounds to hop <= 512)
+  if constexpr (P == 64 && WG == 512 && SH <= 8) {  // (LDS slots: the host limits PR to hop <= 512)
     if (A.yprev) {  // pipelined batch (LDS gain rows: gm 1, or gm 2 at hop 512)
       if constexpr (SH == 8) {
         // pipelined adaptive batches (cross-fade lattice: the pure rows in LDS)
