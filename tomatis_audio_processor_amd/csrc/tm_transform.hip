@@ -691,6 +691,14 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
     };
     const __amdgpu_buffer_rsrc_t rnull = mk_rsrc(ys, 0u);
     float wv[SHQ];
+#pragma unroll
+    for (int q = 0; q < SHQ / 4; ++q) {
+      const float4 t4 = reinterpret_cast<const float4*>(s_winv)[q * P + L];
+      wv[4 * q] = t4.x;
+      wv[4 * q + 1] = t4.y;
+      wv[4 * q + 2] = t4.z;
+      wv[4 * q + 3] = t4.w;
+    }
     auto store_out = [&](const cf (&o)[SH], __amdgpu_buffer_rsrc_t r, int so) {
 #pragma unroll
       for (int i = 0; i < SH; ++i) {
@@ -753,15 +761,8 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
         ++cid;
         next_chunk_k = (cid < S.n_chunks - 1) ? next_chunk_k + chunk_k_step : INT64_MAX;
       }
-      // outputs of this frame's first hop: interior 1/sum w^2, output scale, peak
-#pragma unroll
-      for (int q = 0; q < SHQ / 4; ++q) {
-        const float4 t4 = reinterpret_cast<const float4*>(s_winv)[q * P + L];
-        wv[4 * q] = t4.x;
-        wv[4 * q + 1] = t4.y;
-        wv[4 * q + 2] = t4.z;
-        wv[4 * q + 3] = t4.w;
-      }
+      // outputs of this frame's first hop: interior 1/sum w^2 (per lane, loaded
+      // once before the loop), output scale, peak
       float pf = 0.f;
 #pragma unroll
       for (int i = 0; i < SH; ++i) {
