@@ -255,3 +255,36 @@ def Result_nf(p):
         return p.result()
     finally:
         p.pending = pend
+
+
+def test_pipelined_two_pass_ragged_4096():
+    """n_fft 4096 pipelined (xfade) over ragged streams: first runs whose
+    leading output blocks are partial (scaled by the tail), streams shorter
+    than a frame or than one run, a stream's last run with the stream tail;
+    bit-identical to unpipelined passes."""
+    torch, E = _engine()
+    sr = 96000
+    lens = [sr * 30 + 13, 3000, sr * 3 + 1, 4096, sr * 11 + 999, 5000]
+    xs_np = [[synth_stream(61 + i + 5 * k, n, 2, sr) * (1.0, 0.3, 1.2)[k % 3] for i, n in enumerate(lens)]
+             for k in range(3)]
+    ss = E.StreamSet.from_arrays(xs_np[0], sr)
+    xs = [E.StreamSet.from_arrays(a, sr).x.clone() for a in xs_np]
+    kw = dict(gate_ui=50, gate_offset=-90, n_fft=4096, hop=1024, xfade_ms=500.0)
+    ref = E.GatePipeline(ss, **kw)
+    refs = []
+    for x in xs:
+        ss.x.copy_(x)
+        ref.run()
+        refs.append((ref.y.clone(), ref.peaks.clone(), ref.r.clone(), ref.states.clone()))
+    del ref
+    pipe = E.GatePipeline(ss, pipelined=True, **kw)
+    F = pipe.plan.total_frames
+    held = None
+    for k, x in enumerate(xs):
+        ss.x.copy_(x)
+        assert pipe.run() is None and pipe.pending and pipe.pipelined
+        if held is not None:
+            _check(torch, F, (held[0].clone(), held[1].clone(), held[2], held[3]), refs[k - 1], k - 1)
+        held = (pipe.y, pipe.peaks, pipe.r.clone(), pipe.states.clone())
+    res = pipe.result()
+    _check(torch, F, (res.y, res.chunk_peaks, held[2], held[3]), refs[-1], len(xs) - 1)
