@@ -162,6 +162,14 @@ def test_pipelined_declines():
         pipe = E.GatePipeline(ss, gate_ui=50, pipelined=True, **kw)
         res = pipe.run()
         assert res is not None and not pipe.pending and not pipe.pipelined, kw
+    # 4 channels take the LDS-FFT path (no partner-rescale instantiation)
+    x4 = [synth_stream(77, n, 4, sr)]
+    ss4 = E.StreamSet.from_arrays(x4, sr)
+    ref = E.GatePipeline(ss4, gate_ui=50, n_fft=2048, hop=512).run()
+    pipe = E.GatePipeline(ss4, gate_ui=50, n_fft=2048, hop=512, pipelined=True)
+    res = pipe.run()
+    assert res is not None and not pipe.pending and not pipe.pipelined
+    assert torch.equal(res.y, ref.y) and torch.equal(res.chunk_peaks, ref.chunk_peaks)
 
 
 @pytest.mark.parametrize("case", [
