@@ -45,6 +45,14 @@ WORKLOADS = {
     "c4h": (64, 300, 48000, 2, "standard", 2048, 512,
             "C4 + one hovering stream: 64 x 5 min stereo 48 kHz per GPU, stream 17 a "
             "1 kHz sine at the gate threshold (-40 dBFS), standard, 2048/512"),
+    # the whole 512-stream C4 batch on ONE GPU (14.4 M frames: more than the
+    # 2048 resident run slots x 4096 frames, so runs take two rounds and every
+    # look-back still chains), clean and with the hovering stream 17
+    "c4all": (512, 300, 48000, 2, "standard", 2048, 512,
+              "C4 whole batch on one GPU: 512 x 5 min stereo 48 kHz, standard, 2048/512"),
+    "c4allh": (512, 300, 48000, 2, "standard", 2048, 512,
+               "C4 whole batch on one GPU + one hovering stream: 512 x 5 min stereo 48 kHz, "
+               "stream 17 a 1 kHz sine at the gate threshold (-40 dBFS), standard, 2048/512"),
     "c5x": (16, 300, 96000, 2, "xfade", 4096, 1024,
             "C5 stage 1: 16 x 5 min stereo 96 kHz per GPU, xfade 500 ms, 4096/1024"),
     "c3": (64, 300, 44100, 2, "adaptive", 2048, 512,
@@ -120,7 +128,10 @@ class ChainC5:
         return None
 
     def finish(self):
-        return self.s1.finish() | max(p.finish() for p in self.s2.values())
+        bits = self.s1.finish()
+        for p in self.s2.values():  # (error bits OR together: distinct bits survive)
+            bits |= p.finish()
+        return bits
 
     def result(self):
         return self.s1.result()
@@ -318,6 +329,12 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true",
                     help="standard / adaptive: every pass applies its own limiter (no batch "
                          "pipeline: tomatis_stft_ola_gated / _limited instead of _pipelined)")
+    ap.add_argument("--inputs", type=int, default=2,
+                    help="distinct synthetic inputs of the workload's shape, used in turn by the "
+                         "passes (a pipeline of different files, not one file re-processed)")
+    ap.add_argument("--single-steps", type=int, default=10,
+                    help="also time this many unpipelined passes (a job of ONE file: the limiter "
+                         "ends the pass) with their own pipeline; 0 disables")
     ap.add_argument("--dev", action="append", default=[], metavar="NAME=VALUE",
                     help="development override (TOMATIS_DEV_<NAME>, A/B experiments); "
                          "recorded in the JSON line's config")
@@ -352,34 +369,61 @@ def main():
         ss = engine.StreamSet.synthetic(nstr, n, ch, sr, seed0=1000 + rank * nstr)
         if a.input_gain != 1.0:
             ss.x = engine.scale_copy(ss.x, a.input_gain)
-        if a.workload == "c4h":
+        if a.workload in ("c4h", "c4allh"):
             o, amp = ss.offs[17], np.sqrt(2.0) * 10.0 ** (-40.0 / 20.0)
             t = torch.arange(n, dtype=torch.float64, device="cuda") / sr
             s = (amp * torch.sin(2 * np.pi * 1000.0 * t)).to(torch.float32)
             ss.x[o:o + 2 * n] = torch.stack([s, s], 1).reshape(-1)
-    stages = 1
-    if mode == "standard":
-        # batch pipeline: pass k+1's transform applies pass k's limiter in its
-        # frame loops; the timed region ends with flush() (the last pass's limiter)
-        pipe = engine.GatePipeline(ss, gate_ui=50, n_fft=n_fft, hop=hop,
-                                   pipelined=not a.no_pipeline)
-    elif mode == "xfade":
-        # batch pipeline (two-pass chain, n_fft 4096: the partner blocks through
-        # VGPRs); the timed region ends with flush()
-        pipe = engine.GatePipeline(ss, gate_ui=50, gate_offset=-90, n_fft=n_fft, hop=hop,
-                                   xfade_ms=500.0, pipelined=not a.no_pipeline)
-    elif mode == "adaptive":
-        # two stream groups: one group's host phase overlaps the other's device work
-        # (batch pipeline as in standard mode: the global limiter of pass k in
-        # pass k+1's transforms)
-        pipe = engine.AdaptiveGroups(ss, groups=int(os.environ.get("TOMATIS_C3_GROUPS", "2")),
-                                     n_fft=n_fft, hop=hop, pipelined=not a.no_pipeline)
-    elif mode == "chain":
-        pipe = ChainC5(engine, ss, sr, n_fft, hop, pipelined=not a.no_pipeline)
-        stages = 2
+    # the passes take distinct inputs in turn (seeds differ): input 0 is the one
+    # generated above, the others fresh buffers of the same geometry.  HBM
+    # budget (80 % of the device): inputs + two pipelined outputs + the one-file
+    # pipeline's output; the extras go first when a workload does not fit
+    set_bytes = 4 * n * ch * nstr
+    budget = 0.8 * torch.cuda.get_device_properties(torch.cuda.current_device()).total_memory
+    if (a.inputs + 3) * set_bytes > budget:
+        a.single_steps = 0
+    a.inputs = int(max(1, min(a.inputs, budget // set_bytes - (3 if a.single_steps else 2))))
+    inputs = [ss.x]
+    if mode != "timeshard":
+        for j in range(1, max(1, a.inputs)):
+            o = engine.StreamSet.synthetic(nstr, n, ch, sr, seed0=1000 + rank * nstr + 7919 * j)
+            inputs.append(engine.scale_copy(o.x, a.input_gain) if a.input_gain != 1.0 else o.x)
+            if a.workload in ("c4h", "c4allh"):
+                inputs[-1][ss.offs[17]:ss.offs[17] + 2 * n] = ss.x[ss.offs[17]:ss.offs[17] + 2 * n]
+    stages = 2 if mode == "chain" else 1
+
+    def make_pipe(pipelined):
+        if mode == "standard":
+            # batch pipeline: pass k+1's transform applies pass k's limiter in its
+            # frame loops; the timed region ends with flush() (the last pass's limiter)
+            return engine.GatePipeline(ss, gate_ui=50, n_fft=n_fft, hop=hop, pipelined=pipelined)
+        if mode == "xfade":
+            # batch pipeline (two-pass chain, n_fft 4096: the partner blocks through
+            # VGPRs); the timed region ends with flush()
+            return engine.GatePipeline(ss, gate_ui=50, gate_offset=-90, n_fft=n_fft, hop=hop,
+                                       xfade_ms=500.0, pipelined=pipelined)
+        if mode == "adaptive":
+            # two stream groups: one group's host phase overlaps the other's device
+            # work (batch pipeline as in standard mode: the global limiter of pass k
+            # in pass k+1's transforms)
+            return engine.AdaptiveGroups(ss, groups=int(os.environ.get("TOMATIS_C3_GROUPS", "2")),
+                                         n_fft=n_fft, hop=hop, pipelined=pipelined)
+        if mode == "chain":
+            return ChainC5(engine, ss, sr, n_fft, hop, pipelined=pipelined)
+        return pipe  # timeshard: built above
+
+    pipe = make_pipe(not a.no_pipeline)
     torch.cuda.synchronize()
 
-    for _ in range(a.warmup):
+    def set_input(p, k):
+        """pass k of pipeline p reads input k mod len(inputs)"""
+        if len(inputs) < 2:
+            return
+        for q in getattr(p, "pipes", None) or [getattr(p, "s1", p)]:
+            q.ss.x = inputs[k % len(inputs)]
+
+    for w in range(a.warmup):
+        set_input(pipe, w)
         pipe.run()          # device error word checked after every warm-up pass
     if hasattr(pipe, "flush"):
         pipe.flush()        # pipelined: the timed region starts with nothing pending
@@ -396,6 +440,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(a.steps):
+        set_input(pipe, k)
         pipe.run(marks=marks[k], check_device=False)
     if hasattr(pipe, "flush"):
         pipe.flush()        # pipelined: the last pass's limiter, inside the timed region
@@ -414,6 +459,56 @@ def main():
         tt = torch.tensor([elapsed, kern_ms, dev_err], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed, kern_ms, dev_err = float(tt[0]), float(tt[1]), int(tt[2])
+
+    # HBM copy bandwidth measured in this process (roofline.achievable_peak,
+    # SURVEY §8(d)): the timed launch's input copied by tomatis_copy_probe
+    from tomatis_audio_processor_amd._lib import check as _check, lib as _lib, ptr as _ptr, stream_handle
+    cp_src = inputs[0][: min(inputs[0].numel() // 4, 1 << 27) * 4]  # <= 2 GiB, >> the MALL
+    cp_dst = torch.empty_like(cp_src)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    for j in range(7):
+        if j == 2:
+            ev[0].record()
+        _check(_lib().tomatis_copy_probe(_ptr(cp_src), _ptr(cp_dst), cp_src.numel(), stream_handle()),
+               "copy_probe")
+    ev[1].record()
+    torch.cuda.synchronize()
+    copy_gbs = 2.0 * 4.0 * cp_src.numel() * 5 / (ev[0].elapsed_time(ev[1]) * 1e-3) / 1e9
+    del cp_dst
+
+    # a job of ONE file: unpipelined passes of the same workload (each ends with
+    # its own limiter), their own pipeline; the headline above is a pipeline of
+    # distinct files (pass k+1 limits pass k inside its transform), as batch.py
+    # runs a multi-file job
+    one = None
+    if a.single_steps > 0 and not strong and not a.no_pipeline:
+        p1 = make_pipe(False)
+        for w in range(2):
+            set_input(p1, w)
+            p1.run()
+        torch.cuda.synchronize()
+        if ws > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for k in range(a.single_steps):
+            set_input(p1, k)
+            p1.run(check_device=False)
+        torch.cuda.synchronize()
+        if ws > 1:
+            dist.barrier()
+        el1 = time.perf_counter() - t0
+        for pl in plans_of(p1):
+            dev_err |= pl.error_bits()
+        if ws > 1:
+            tt = torch.tensor([el1], dtype=torch.float64, device="cuda")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el1 = float(tt[0])
+        one = {"ms_per_step": round(el1 / a.single_steps * 1e3, 4),
+               "value": round(n * ch * nstr * ws * a.single_steps / el1 / 1e6, 1),
+               "unit": "Msamples/s", "steps": a.single_steps,
+               "what": "one file per job: unpipelined passes (each pass applies its own "
+                       "limiter), no previous file to overlap with"}
+        del p1
 
     # per-stream manifest: (rank, stream, frames, C2 frames, max chunk peak bits)
     res = pipe.result()
@@ -455,7 +550,9 @@ def main():
             "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (seeded device-generated noise, -20/-60 dBFS alternating 1.5 s)"
-                    + (f", x{a.input_gain:g}" if a.input_gain != 1.0 else ""),
+                    + (f", x{a.input_gain:g}" if a.input_gain != 1.0 else "")
+                    + (f"; {len(inputs)} distinct inputs taken in turn by the passes"
+                       if len(inputs) > 1 else ""),
             "config": {"workload": desc, "streams_per_gpu": nstr, "samples_per_channel": n,
                        "channels": ch, "sr": sr, "mode": mode, "n_fft": n_fft, "hop": hop,
                        "parallelism": (f"time-sharded x{ws} (RCCL gate all_gather + peak "
@@ -468,6 +565,10 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "achievable_peak": round(copy_gbs, 1),
+                         "frac_achievable": round(achieved_gbs / copy_gbs, 4),
+                         "achievable_how": "tomatis_copy_probe (16-byte streaming copy) of the "
+                                           "launch's input in this process, read + write bytes",
                          "kernel": "k_stft_ola (fused frame/window/FFT/gain/IFFT/OLA/normalise + per-chunk limiter)",
                          "kernel_ms": round(kern_ms, 4),
                          "alg_bytes_per_launch": alg_bytes},
@@ -476,6 +577,7 @@ def main():
                         "frac": round(tflops / FP32_PEAK_TFLOPS, 4),
                         "flop_per_ch_sample": round(flops_per_ch_sample(n_fft, hop), 1)},
             "device_error": dev_err,
+            "one_file_job": one,
             "cpu_baseline": cpu,
             "manifest": {"streams": int(man.shape[0]),
                          "c2_fraction": round(float(man[:, 3].sum() / max(1, man[:, 2].sum())), 4)},

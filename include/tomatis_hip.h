@@ -62,7 +62,7 @@
 extern "C" {
 #endif
 
-#define TOMATIS_ABI_VERSION 9
+#define TOMATIS_ABI_VERSION 10
 
 #define TOMATIS_OK 0
 #define TOMATIS_E_ARG (-1)        /* bad argument */
@@ -298,6 +298,28 @@ int tomatis_stft_ola_pipelined(tomatis_plan_t plan, const float* x, const float*
                                int32_t n_rows, const uint16_t* rows, float* y,
                                uint32_t* chunk_peak_bits, float limit, float* prev_y,
                                const uint32_t* prev_peak_bits, void* hip_stream);
+/* Batch pipelines over DIFFERENT plans (a multi-file job: batch k+1's files
+ * are not batch k's): as tomatis_stft_ola_gated_pipelined /
+ * tomatis_stft_ola_pipelined, with prev_y / prev_peak_bits written by the
+ * previous call with prev_plan (NULL: this plan).  prev_plan must have this
+ * plan's n_fft, hop and channel count (else TOMATIS_E_UNSUPPORTED: the caller
+ * limits prev_y with tomatis_apply_limiter(prev_plan, ...) and runs this batch
+ * unpipelined).  Run r of this launch scales run r of prev_plan's output in its
+ * frame loop; prev_plan's runs beyond this plan's run count are limited by a
+ * short launch after the transform.  prev_plan must stay alive until the call's
+ * work has completed.  Results are bit-identical to limiting each batch with
+ * its own plan (src/process_tomatis.py:331-357, per file). */
+int tomatis_stft_ola_gated_pipelined_after(tomatis_plan_t plan, const float* x,
+                                           const float* gain_rows, int32_t n_rows, float* y,
+                                           uint32_t* chunk_peak_bits, float limit, float* r_out,
+                                           uint8_t* states_out, tomatis_plan_t prev_plan,
+                                           float* prev_y, const uint32_t* prev_peak_bits,
+                                           void* hip_stream);
+int tomatis_stft_ola_pipelined_after(tomatis_plan_t plan, const float* x, const float* gain_rows,
+                                     int32_t n_rows, const uint16_t* rows, float* y,
+                                     uint32_t* chunk_peak_bits, float limit,
+                                     tomatis_plan_t prev_plan, float* prev_y,
+                                     const uint32_t* prev_peak_bits, void* hip_stream);
 /* The limiter on the edge chunks of edge_mask only. */
 int tomatis_apply_limiter_edges(tomatis_plan_t plan, float* y, const uint32_t* chunk_peak_bits,
                                 float limit, int32_t edge_mask, void* hip_stream);
@@ -349,10 +371,12 @@ int tomatis_plan_set_option(tomatis_plan_t plan, int32_t option, int64_t value);
  * explicit: the library reads no environment variable.  value < 0 restores the
  * default.  Read at plan creation: FORCE_LDS, P64 (n_fft 2048 as one wave per
  * frame), FAST_LOOP (interior loop), RUN_FRAMES (frames per run, 0 auto),
- * RUN_ROUNDS, LEVELS_LEGACY, GATE_TF (transfer-function gate scan), MH_PARTS;
+ * RUN_ROUNDS, LEVELS_LEGACY, GATE_TF (transfer-function gate scan), MH_PARTS,
+ * SLOTS (resident run slots: few slots make long runs on small inputs);
  * at launch: GATE_TF, ALPHA_SEQ (sequential xfade alpha), GAIN_LDS,
- * FUSE_LIMITER, WG (transform workgroup size), FUSED_LEVELS (key 13 is
- * unused).  Results are bit-identical
+ * FUSE_LIMITER, WG (transform workgroup size), FUSED_LEVELS.  Standard-mode
+ * plans at n_fft 2048 cut runs of at most 4096 frames whatever RUN_FRAMES
+ * says (the in-kernel gate's chained look-back).  Results are bit-identical
  * under every value (the decomposition tests vary them). */
 #define TOMATIS_DEV_FAST_LOOP 1
 #define TOMATIS_DEV_RUN_ROUNDS 2
@@ -366,6 +390,7 @@ int tomatis_plan_set_option(tomatis_plan_t plan, int32_t option, int64_t value);
 #define TOMATIS_DEV_GAIN_LDS 10
 #define TOMATIS_DEV_FUSE_LIMITER 11
 #define TOMATIS_DEV_WG 12
+#define TOMATIS_DEV_SLOTS 13           /* resident run slots assumed by the plan (0: the device's) */
 #define TOMATIS_DEV_FUSED_LEVELS 14    /* 0: tomatis_stft_ola_gated declines (host two-pass) */
 int tomatis_set_dev_option(int32_t key, int32_t value);
 /* The current override of key (-1: default, or an unknown key). */
@@ -428,6 +453,12 @@ int tomatis_absmax(const float* x, int64_t n, uint32_t* out_bits, void* hip_stre
  * np.max(np.abs(x)) of src/process_tomatis_adaptive.py:201 for a batch. */
 int tomatis_absmax_streams(tomatis_plan_t plan, const float* x, uint32_t* out_bits,
                            void* hip_stream);
+
+/* HBM bandwidth probe: y = x for n floats (n % 4 == 0, both 16-byte aligned)
+ * with 16-byte streaming loads and stores -- bench.py times it to report the
+ * roofline against a measured copy bandwidth beside the 8 TB/s spec.  Replaces
+ * nothing in the reference. */
+int tomatis_copy_probe(const float* x, float* y, int64_t n, void* hip_stream);
 
 /* y[i] = x[i] * scale (float32), n floats (layer-2 gain-protect copy). */
 int tomatis_scale_copy(const float* x, float* y, int64_t n, float scale, void* hip_stream);

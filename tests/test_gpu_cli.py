@@ -186,3 +186,46 @@ def test_process_tomatis_flac_in_flac_out(tmp_path):
     ref = orc.process_standard(xq, sr, gate_ui=50, n_fft=2048, hop=512)
     m = ref["wsum"][ref["pad"]:ref["pad"] + N] >= 1e-3
     _cmp(y, ref["y"], m)
+
+
+@pytest.mark.parametrize("mode,extra", [("standard", []), ("xfade", []),
+                                        ("adaptive", ["--n_fft", "2048", "--hop", "512"])])
+def test_batch_runner_pipelined_batches(tmp_path, mode, extra):
+    """A rank's files as a pipeline of >= 3 batches of different geometry
+    (--batch_gb small: batch k+1's transform limits batch k's output,
+    tomatis_stft_ola_*_pipelined_after): every output file and the manifest
+    byte-identical to --no_pipeline (each batch limited by itself)."""
+    _gpu()
+    from tomatis_audio_processor_amd import batch
+    import json
+    sr = 48000
+    # 7 files of different lengths, some loud (limited chunks), one short
+    lens = [sr * 9 + 17, sr * 4 + 3, 3000, sr * 12 + 5, sr * 6, sr * 2 + 999, sr * 8 + 1]
+    files = []
+    for i, n in enumerate(lens):
+        x = synth_stream(300 + i, n, 2, sr) * (1.0, 0.3, 1.2)[i % 3]
+        files.append(_wav(tmp_path, f"g{i}.wav", x.astype(np.float32), sr))
+    # ~ 2 files per batch: 14 s of 48 kHz stereo float
+    gb = 14 * sr * 2 * 4 / 2 ** 30
+    args = ["-i", *files, "--mode", mode, "--batch_gb", f"{gb:.9f}", *extra]
+    if mode != "adaptive":
+        args += ["--n_fft", "2048", "--hop", "512"]
+    od1, od2 = str(tmp_path / "p"), str(tmp_path / "u")
+    assert batch.main(args + ["--out_dir", od1]) == 0
+    assert batch.main(args + ["--out_dir", od2, "--no_pipeline"]) == 0
+    ids = list(range(len(lens)))
+    sizes = {i: lens[i] * 2 for i in ids}
+    assert len(batch.split_batches(ids, sizes, int(gb * 2 ** 30 / 4))) >= 3
+    for i in ids:
+        a = open(os.path.join(od1, f"g{i}_tomatis.wav"), "rb").read()
+        b = open(os.path.join(od2, f"g{i}_tomatis.wav"), "rb").read()
+        assert a == b, f"file {i} differs ({mode})"
+    m1 = json.load(open(os.path.join(od1, "manifest.json")))
+    m2 = json.load(open(os.path.join(od2, "manifest.json")))
+    assert m1 == m2
+    if mode == "standard":  # and the oracle on a limited file of the middle batch
+        x = (synth_stream(303, lens[3], 2, sr) * 1.0).astype(np.float32)  # (FLOAT WAV: exact)
+        y, _ = audio_io.read(os.path.join(od1, "g3_tomatis.wav"))
+        ref = orc.process_standard(x, sr, gate_ui=50, n_fft=2048, hop=512)
+        N = lens[3]
+        _cmp(y, ref["y"], ref["wsum"][ref["pad"]:ref["pad"] + N] >= 1e-3)

@@ -284,3 +284,39 @@ def test_gated_level_sweeps_through_thresholds():
     pipe, ref = _pair(E, ss, gate_ui=50, n_fft=2048, hop=hop)
     assert pipe.gated_used and pipe.gate_fallbacks == 0
     _assert_same(torch, pipe, ref)
+
+
+@pytest.mark.parametrize("opts", [
+    # 8 x 5 min 48 kHz on 64 run slots: 56 interior slots want ~4000-frame runs;
+    # more than 4096 frames per slot would break the chain, so the plan cuts
+    # two rounds of runs
+    dict(SLOTS=64),
+    # an explicit 8192-frame request is capped at 4096 all the same
+    dict(SLOTS=64, RUN_FRAMES=8192),
+    # the same with a single run slot per stream's worth: many rounds
+    dict(SLOTS=16),
+])
+def test_gated_hovering_long_runs(opts):
+    """A batch whose frames exceed slots x 4096 (SURVEY C4's 512 streams on one
+    GPU are 14.4 M frames on 2048 slots; TOMATIS_DEV_SLOTS reproduces the ratio
+    on 8 streams) with one stream hovering at the threshold for all 5 minutes:
+    runs stay within the chained look-back (tm_kernels.hip build_runs), the pass
+    takes the fused gate with no two-pass fallback, bit-identical to the
+    two-pass chain (src/process_tomatis.py:373-385 has no look-back horizon)."""
+    torch, E = _engine()
+    sr = 48000
+    n = 300 * sr
+    with _dev_opts(**opts):
+        ss = E.StreamSet.synthetic(8, n, 2, sr, seed0=1000)
+        o = ss.offs[3]
+        ss.x[o:o + 2 * n] = torch.from_numpy(_hover(n, sr).reshape(-1)).to(ss.x.device)
+        pipe, ref = _pair(E, ss, gate_ui=50, n_fft=2048, hop=512)
+        assert pipe.gated_used and pipe.gate_fallbacks == 0, opts
+        _assert_same(torch, pipe, ref)
+        # pipelined passes of the same long-run plan: no fallback either
+        pp = E.GatePipeline(ss, gate_ui=50, n_fft=2048, hop=512, pipelined=True)
+        pp.run()
+        pp.run()
+        res = pp.result()
+        assert pp.gate_fallbacks == 0
+        assert torch.equal(res.y, ref[0]) and torch.equal(res.chunk_peaks, ref[3])

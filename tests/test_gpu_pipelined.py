@@ -296,3 +296,103 @@ def test_pipelined_two_pass_ragged_4096():
         held = (pipe.y, pipe.peaks, pipe.r.clone(), pipe.states.clone())
     res = pipe.result()
     _check(torch, F, (res.y, res.chunk_peaks, held[2], held[3]), refs[-1], len(xs) - 1)
+
+
+@pytest.mark.parametrize("case", [
+    # (name, kw, batches: list of (seconds per stream), per-batch gain)
+    ("std_2048", dict(gate_ui=50, n_fft=2048, hop=512),
+     [[300], [40, 7, 61], [2, 3], [120, 120, 30, 1], [600]]),
+    ("std_mono_hop256", dict(gate_ui=50, n_fft=2048, hop=256, ch=1),
+     [[50, 9], [200], [1, 33, 4]]),
+    ("xfade_4096", dict(gate_ui=50, gate_offset=-90, n_fft=4096, hop=1024, xfade_ms=500.0, sr=96000),
+     [[60, 11], [3], [90, 45, 20]]),
+    ("xfade_2048", dict(gate_ui=50, gate_offset=-90, n_fft=2048, hop=512, xfade_ms=500.0),
+     [[30], [70, 5], [12, 12, 12]]),
+])
+def test_pipelined_across_plans(case):
+    """A pipeline of batches with DIFFERENT plans (a multi-file job: batch.py):
+    GatePipeline.run(prev_pipe=...) limits the previous batch's output inside
+    this batch's transform (tomatis_stft_ola_*_pipelined_after) -- partner run r
+    of another plan, and that plan's runs beyond this one's run count in the
+    follow-up launch (a long batch followed by a short one and vice versa).
+    Every batch's output and peaks equal the batch processed alone, bit for bit."""
+    torch, E = _engine()
+    name, kw, batches = case
+    kw = dict(kw)
+    ch, sr = kw.pop("ch", 2), kw.pop("sr", 44100)
+    sss, refs = [], []
+    for b, secs in enumerate(batches):
+        arrays = [synth_stream(500 + 13 * b + i, s * sr + 7 * i + 1, ch, sr) * (1.0, 0.4, 1.3)[(b + i) % 3]
+                  for i, s in enumerate(secs)]
+        ss = E.StreamSet.from_arrays(arrays, sr)
+        sss.append(ss)
+        res = E.GatePipeline(ss, **kw).run()
+        refs.append((res.y.clone(), res.chunk_peaks.clone(), res.states.clone()))
+    prev = None
+    for b, ss in enumerate(sss):
+        pipe = E.GatePipeline(ss, pipelined=True, second_buffer=False, **kw)
+        assert pipe.run(prev_pipe=prev) is None and pipe.pending and pipe.pipelined
+        F = pipe.plan.total_frames
+        assert torch.equal(pipe.states[:F], refs[b][2][:F]), f"batch {b}: states"
+        if prev is not None:
+            assert not prev.pending, "the previous batch is limited by this launch"
+            res = prev.result()
+            assert torch.equal(res.chunk_peaks, refs[b - 1][1]), f"batch {b - 1}: peaks"
+            assert torch.equal(res.y, refs[b - 1][0]), f"batch {b - 1}: output"
+            assert prev._ys[1] is None, "one output buffer per single-pass pipeline"
+        prev = pipe
+    res = prev.result()
+    assert torch.equal(res.y, refs[-1][0]) and torch.equal(res.chunk_peaks, refs[-1][1])
+
+
+def test_pipelined_across_plans_declines():
+    """A previous batch of another shape (hop 256 after hop 512) cannot be
+    limited by this launch: it is flushed on its own plan, and this batch still
+    pipelines; results bit-identical."""
+    torch, E = _engine()
+    sr = 44100
+    a = E.StreamSet.from_arrays([synth_stream(900, sr * 50, 2, sr)], sr)
+    b = E.StreamSet.from_arrays([synth_stream(901, sr * 30, 2, sr) * 1.2], sr)
+    ra = E.GatePipeline(a, gate_ui=50, n_fft=2048, hop=512).run()
+    ya = ra.y.clone()
+    rb = E.GatePipeline(b, gate_ui=50, n_fft=2048, hop=256).run()
+    yb = rb.y.clone()
+    pa = E.GatePipeline(a, gate_ui=50, n_fft=2048, hop=512, pipelined=True)
+    pa.run()
+    pb = E.GatePipeline(b, gate_ui=50, n_fft=2048, hop=256, pipelined=True)
+    pb.run(prev_pipe=pa)
+    assert not pa.pending and pb.pending
+    assert torch.equal(pa.result().y, ya)
+    assert torch.equal(pb.result().y, yb)
+
+
+def test_pipelined_adaptive_across_plans():
+    """AdaptiveGroups batches of different plans: group g of batch k+1 limits
+    group g of batch k (global limiter of src/process_tomatis_adaptive.py:
+    340-345 inside the next transform); a 1-group batch after a 2-group one
+    flushes the group it has no partner for."""
+    torch, E = _engine()
+    sr = 44100
+    specs = [[40, 20, 33, 10, 5, 61], [12, 70, 3, 9], [25, 25]]
+    sss, refs = [], []
+    for b, secs in enumerate(specs):
+        arrays = [synth_stream(700 + 17 * b + i, s * sr + 3 * i, 2, sr) * (1.0, 0.2, 1.4)[(i + b) % 3]
+                  for i, s in enumerate(secs)]
+        ss = E.StreamSet.from_arrays(arrays, sr)
+        sss.append(ss)
+        g = 2 if len(secs) >= 4 else 1
+        res = E.AdaptiveGroups(ss, groups=g, n_fft=2048, hop=512).run()
+        refs.append((res.y.clone(), res.chunk_peaks.clone()))
+    prev = None
+    for b, ss in enumerate(sss):
+        g = 2 if len(specs[b]) >= 4 else 1
+        pipe = E.AdaptiveGroups(ss, groups=g, n_fft=2048, hop=512, pipelined=True)
+        assert pipe.run(prev_pipe=prev) is None and pipe.pending
+        if prev is not None:
+            assert not prev.pending
+            res = prev.result()
+            assert torch.equal(res.chunk_peaks, refs[b - 1][1]), f"batch {b - 1}: peaks"
+            assert torch.equal(res.y, refs[b - 1][0]), f"batch {b - 1}: output"
+        prev = pipe
+    res = prev.result()
+    assert torch.equal(res.y, refs[-1][0])

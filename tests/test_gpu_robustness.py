@@ -116,7 +116,9 @@ def test_pair_barrier_bit_raises():
 
 
 def test_c3_batch_as_benched():
-    """bench.py --workload c3: 64 x 5 min, AdaptiveGroups(2), seeds 1000.."""
+    """bench.py --workload c3's one-file-job leg (``one_file_job``: unpipelined
+    passes, the global limiter inside each pass): 64 x 5 min, AdaptiveGroups(2),
+    seeds 1000..  The pipelined mode of the headline: test_gpu_as_benched.py."""
     torch, E = _engine()
     sr, n, S = 44100, 300 * 44100, 64
     n_fft, hop = 2048, 512
@@ -153,7 +155,9 @@ def test_c3_batch_as_benched():
 
 
 def test_c4_batch_per_gpu():
-    """bench.py --workload c4 (one GPU's share of C4): 64 x 5 min 48 kHz."""
+    """bench.py --workload c4's one-file-job leg (one GPU's share of C4,
+    unpipelined: the fused limiter tail): 64 x 5 min 48 kHz.  The pipelined
+    mode of the headline: test_gpu_as_benched.py."""
     torch, E = _engine()
     sr, n, S = 48000, 300 * 48000, 64
     ss = E.StreamSet.synthetic(S, n, 2, sr, seed0=1000)
@@ -189,7 +193,7 @@ def test_c4_batch_per_gpu():
 
 
 def test_c5_batch_per_gpu():
-    """bench.py --workload c5 exactly as timed (one GPU's share of C5): 16 x
+    """bench.py --workload c5, one pass + flush (one GPU's share of C5): 16 x
     5 min stereo 96 kHz, xfade 500 ms (4096/1024) -> layer-2b residual EQ
     (bench.ChainC5).  Stage 1: the per-chunk limiter property on all 16 streams;
     4 streams vs orc.process_standard(xfade_ms=500) -- states and alpha bit-exact,

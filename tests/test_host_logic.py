@@ -224,3 +224,16 @@ def test_levels_threaded_inside_host_pool_no_deadlock(monkeypatch):
     fut = engine._host_pool().submit(engine._levels_threaded, r, out)
     fut.result(timeout=60)
     assert np.array_equal(out, dsp.r_to_level(r))
+
+
+def test_split_batches():
+    """batch.py cuts a rank's files into consecutive batches within the input
+    budget; an oversize file is a batch of its own; every id once, in order."""
+    from tomatis_audio_processor_amd.batch import split_batches
+    sizes = {0: 5, 1: 3, 2: 9, 3: 20, 4: 1, 5: 1, 6: 7}
+    b = split_batches(list(range(7)), sizes, 10)
+    assert b == [[0, 1], [2], [3], [4, 5, 6]]
+    assert [i for x in b for i in x] == list(range(7))
+    assert split_batches([], sizes, 10) == []
+    assert split_batches([3], sizes, 1) == [[3]]
+    assert split_batches([4, 5], sizes, 100) == [[4, 5]]

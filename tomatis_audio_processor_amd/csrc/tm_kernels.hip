@@ -1546,6 +1546,25 @@ __global__ __launch_bounds__(256) void k_scale_copy(const float* __restrict__ x,
     y[i] = x[i] * s;
 }
 
+// HBM bandwidth probe (bench.py's roofline.achievable_peak):
+// y = x as 16-byte streaming loads / stores, 4 in flight per lane
+__global__ __launch_bounds__(256) void k_copy_probe(const float4* __restrict__ x,
+                                                    float4* __restrict__ y, int64_t n4) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const f4v* xv = reinterpret_cast<const f4v*>(x);
+  f4v* yv = reinterpret_cast<f4v*>(y);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n4; i += 4 * stride) {
+    f4v t[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) t[u] = __builtin_nontemporal_load(xv + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) __builtin_nontemporal_store(t[u], yv + i + u * stride);
+  }
+  for (; i < n4; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(xv + i), yv + i);
+}
+
 // PCM <-> float at the file boundary, libsndfile's
 // normalisation as audio_io implements it: int -> float divides by 2^(bps-1)
 // (correctly rounded: double division, then float); float -> int multiplies by
@@ -1862,14 +1881,24 @@ static int build_runs(tomatis_plan_s* p) {
     if (hipGetDevice(&dev) == hipSuccess)
       (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     slots = (int64_t)std::max(1, ncu) * (p->generic ? 8 : transform_slots_per_cu(P, p->NR));
+    const int dslots = dev_opt(TOMATIS_DEV_SLOTS, 0);  // tests: long runs on small inputs
+    if (dslots > 0) slots = dslots;
   }
   p->run_slots = slots;
+  // Runs the in-kernel gate may take (tomatis_stft_ola_gated: standard mode at
+  // n_fft 2048) are at most kGateLookbackMax frames, so every run's look-back
+  // can chain to its predecessor's carry (k_gate_carry): a batch larger than
+  // slots x kGateLookbackMax frames gets more rounds of runs instead of longer
+  // runs, and a stream hovering inside the hysteresis band never sends the
+  // pass back to the two-pass chain (src/process_tomatis.py:373-385 has no
+  // horizon either)
+  const bool gate_runs = d.alpha_mode == 0 && N == 2048 && P == 64 && !p->generic && !p->lds;
   // rounds: the runs fill the slots this many times over, in stream/position
   // order, so (in-order dispatch) early streams and chunks complete while later
   // runs still compute, and their limiter rescale overlaps that compute
   // (adaptive: every stream is one limiter chunk, measured 1.4 ms faster on C3
   // with 2 rounds; standard 10 s chunks gain nothing and pay warm-up frames)
-  const int rounds = std::max(1, dev_opt(TOMATIS_DEV_RUN_ROUNDS, (d.alpha_mode == 2 && ns > 1) ? 2 : 1));
+  int rounds = std::max(1, dev_opt(TOMATIS_DEV_RUN_ROUNDS, (d.alpha_mode == 2 && ns > 1) ? 2 : 1));
   int T = dev_opt(TOMATIS_DEV_RUN_FRAMES, 0);
   if (T <= 0) {
     // generic streams and the edge runs take slots first
@@ -1877,6 +1906,10 @@ static int build_runs(tomatis_plan_s* p) {
     for (int s = 0; s < ns; ++s)
       if (e_lo[s] == e_hi[s]) gen_frames += p->hs[s].n_frames;
     const int64_t work = fast_total + gen_frames;
+    if (gate_runs) {  // enough rounds that runs stay within the chained look-back
+      const int64_t per_round = std::max<int64_t>(1, slots - n_edge) * (int64_t)(kGateLookbackMax - 64);
+      rounds = (int)std::max<int64_t>(rounds, (work + per_round - 1) / per_round);
+    }
     const int64_t avail = std::max<int64_t>(1, rounds * slots - n_edge);
     T = (int)std::max<int64_t>(rounds > 1 ? 32 : 48, (work + avail - 1) / avail);
     auto count = [&](int64_t t) {
@@ -1890,6 +1923,7 @@ static int build_runs(tomatis_plan_s* p) {
     while (count(T) > rounds * slots && T < tf_total) T += std::max(1, T / 64);
   }
   T = std::min(T, 1 << 20);  // interior buffer resources stay far below 4 GB
+  if (gate_runs) T = std::min(T, kGateLookbackMax);
   std::vector<Run> runs;
   auto add_runs = [&](int s, int64_t a0, int64_t a1, int32_t flags) {
     // equal cuts of [a0, a1) into ceil(len / T) runs
@@ -2655,6 +2689,7 @@ static int gate_lookback(tomatis_plan_s* p, const float* x, hipStream_t s) {
 struct PrevBatch {
   float* y;               // its unscaled output (nullptr: first batch)
   const uint32_t* peaks;  // its final chunk peaks
+  const tomatis_plan_s* plan;  // its plan (this plan, or one of the same shape)
 };
 
 // piece lists of the pipelined partner rescale: every run's own emitted blocks
@@ -2784,6 +2819,10 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
   A.gwin = nullptr;
   A.yprev = nullptr;
   A.peaks_prev = nullptr;
+  A.runs_prev = p->runs;
+  A.st_prev = p->st;
+  A.chunk_rng_prev = p->chunk_rng;
+  A.n_runs_prev = p->n_runs;
   if (gate) {
     // per run: the carry-in state id and leaf window (k_gate_carry), then the
     // transform computes every frame's r and state from the input it loads
@@ -2827,6 +2866,10 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
       if (rc) return rc;
       A.yprev = prev->y;
       A.peaks_prev = prev->peaks;
+      A.runs_prev = prev->plan->runs;
+      A.st_prev = prev->plan->st;
+      A.chunk_rng_prev = prev->plan->chunk_rng;
+      A.n_runs_prev = prev->plan->n_runs;
       A.pieces = p->xs_pieces;
       A.max_pieces = p->xs_max_pieces;
       launch_r2_plan(A, p->xs_pieces, p->total_chunks, p->P, s);  // (zeroes this launch's peaks)
@@ -2835,6 +2878,9 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
       return TOMATIS_E_HIP;
     }
     launch_transform(A, p->P, p->NR, p->SH, ch, transform_wg(p->P, p->NR), s);
+    int rc = launch_check();
+    if (rc) return rc;
+    launch_prev_runs(A, N, s);  // the previous plan's runs this launch has no partner for
     return launch_check();
   }
 #ifdef TM_PROFILE
@@ -2956,10 +3002,20 @@ int tomatis_stft_ola_gated_after_lookback(tomatis_plan_t p, const float* x, cons
   return stft_ola_gated(p, x, gains, n_rows, y, peaks, limit, r_out, states_out, true, hs);
 }
 
-int tomatis_stft_ola_gated_pipelined(tomatis_plan_t p, const float* x, const float* gains,
-                                     int32_t n_rows, float* y, uint32_t* peaks, float limit,
-                                     float* r_out, uint8_t* states_out, float* prev_y,
-                                     const uint32_t* prev_peaks, void* hs) {
+// a previous batch another plan wrote can be limited by this plan's launch
+// when the partner rescale's block geometry is the same (n_fft, hop, channels,
+// kernel shape) and that plan has per-chunk output ranges
+static bool prev_plan_ok(const tomatis_plan_s* p, const tomatis_plan_s* q) {
+  if (q == p) return true;
+  return q->d.n_fft == p->d.n_fft && q->d.hop == p->d.hop && q->d.ch == p->d.ch && q->P == p->P &&
+         q->NR == p->NR && q->SH == p->SH && !q->generic && !q->lds && q->chunk_rng &&
+         q->total_chunks > 0;
+}
+
+int tomatis_stft_ola_gated_pipelined_after(tomatis_plan_t p, const float* x, const float* gains,
+                                           int32_t n_rows, float* y, uint32_t* peaks, float limit,
+                                           float* r_out, uint8_t* states_out, tomatis_plan_t prev_plan,
+                                           float* prev_y, const uint32_t* prev_peaks, void* hs) {
   if (!p || !x || !gains || !y || !peaks || !r_out || !states_out || n_rows != 2 ||
       !(limit > 0.f) || (prev_y && (!prev_peaks || prev_y == y || prev_peaks == peaks)))
     return TOMATIS_E_ARG;
@@ -2967,14 +3023,32 @@ int tomatis_stft_ola_gated_pipelined(tomatis_plan_t p, const float* x, const flo
   // hop <= 512 (gated_eligible), per-chunk accounting
   if (!gated_eligible(p) || p->total_chunks <= 0 || !p->chunk_need || p->SH > 8)
     return TOMATIS_E_UNSUPPORTED;
+  const tomatis_plan_s* q = prev_plan ? prev_plan : p;
+  if (prev_y && !prev_plan_ok(p, q)) return TOMATIS_E_UNSUPPORTED;
   const GateOut g{r_out, states_out, true};
-  const PrevBatch pb{prev_y, prev_peaks};
+  const PrevBatch pb{prev_y, prev_peaks, q};
   return stft_ola_impl(p, x, gains, n_rows, nullptr, y, peaks, limit, hs, &g, &pb);
+}
+
+int tomatis_stft_ola_gated_pipelined(tomatis_plan_t p, const float* x, const float* gains,
+                                     int32_t n_rows, float* y, uint32_t* peaks, float limit,
+                                     float* r_out, uint8_t* states_out, float* prev_y,
+                                     const uint32_t* prev_peaks, void* hs) {
+  return tomatis_stft_ola_gated_pipelined_after(p, x, gains, n_rows, y, peaks, limit, r_out,
+                                                states_out, nullptr, prev_y, prev_peaks, hs);
 }
 
 int tomatis_stft_ola_pipelined(tomatis_plan_t p, const float* x, const float* gains,
                                int32_t n_rows, const uint16_t* rows, float* y, uint32_t* peaks,
                                float limit, float* prev_y, const uint32_t* prev_peaks, void* hs) {
+  return tomatis_stft_ola_pipelined_after(p, x, gains, n_rows, rows, y, peaks, limit, nullptr,
+                                          prev_y, prev_peaks, hs);
+}
+
+int tomatis_stft_ola_pipelined_after(tomatis_plan_t p, const float* x, const float* gains,
+                                     int32_t n_rows, const uint16_t* rows, float* y,
+                                     uint32_t* peaks, float limit, tomatis_plan_t prev_plan,
+                                     float* prev_y, const uint32_t* prev_peaks, void* hs) {
   if (!p || !x || !gains || !rows || !y || !peaks || n_rows < 1 || !(limit > 0.f) ||
       (prev_y && (!prev_peaks || prev_y == y || prev_peaks == peaks)))
     return TOMATIS_E_ARG;
@@ -2990,7 +3064,9 @@ int tomatis_stft_ola_pipelined(tomatis_plan_t p, const float* x, const float* ga
   if (p->generic || p->lds || p->NR != 32 || p->SH > 8 || !(p64 || p128) ||
       p->total_chunks <= 0 || !p->chunk_need)
     return TOMATIS_E_UNSUPPORTED;
-  const PrevBatch pb{prev_y, prev_peaks};
+  const tomatis_plan_s* q = prev_plan ? prev_plan : p;
+  if (prev_y && !prev_plan_ok(p, q)) return TOMATIS_E_UNSUPPORTED;
+  const PrevBatch pb{prev_y, prev_peaks, q};
   return stft_ola_impl(p, x, gains, n_rows, rows, y, peaks, limit, hs, nullptr, &pb);
 }
 
@@ -3081,6 +3157,21 @@ int tomatis_scale_copy(const float* x, float* y, int64_t n, float scale, void* h
   if (n == 0) return TOMATIS_OK;
   const unsigned g = (unsigned)std::min<int64_t>(4096, (n + 1023) / 1024);
   hipLaunchKernelGGL(k_scale_copy, dim3(g), dim3(256), 0, (hipStream_t)hs, x, y, n, scale);
+  return launch_check();
+}
+
+int tomatis_copy_probe(const float* x, float* y, int64_t n, void* hs) {
+  if (!x || !y || n < 0 || (n & 3) || ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15))
+    return TOMATIS_E_ARG;
+  const int64_t n4 = n / 4;
+  if (n4 == 0) return TOMATIS_OK;
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess)
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  // 8 blocks per CU, each lane 4 x 16 bytes per trip
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((int64_t)ncu * 8, (n4 + 1023) / 1024));
+  hipLaunchKernelGGL(k_copy_probe, dim3(g), dim3(256), 0, (hipStream_t)hs,
+                     reinterpret_cast<const float4*>(x), reinterpret_cast<float4*>(y), n4);
   return launch_check();
 }
 

@@ -71,6 +71,15 @@ struct MainArgs {
   // kernel's own output stays unscaled (defer_self) for the next batch.
   float* yprev;
   const uint32_t* peaks_prev;
+  // the previous batch's plan (tomatis_stft_ola_*_pipelined_after: any plan of
+  // the same n_fft / hop / channels; else this plan's own arrays): its runs,
+  // stream table and chunk output ranges.  Run r's partner is run r of that
+  // plan when r < n_runs_prev; partner runs >= n_runs are limited by
+  // launch_prev_runs after the transform
+  const Run* runs_prev;
+  const TomatisStream* st_prev;
+  const int64_t* chunk_rng_prev;
+  int n_runs_prev;
   // gain rows as the caller passed them ([rows][n_bins], not permuted): when
   // set, the LDS-gain prologue (all rows in LDS) permutes them itself and the
   // host launches no k_gain_perm
@@ -89,6 +98,9 @@ struct MainArgs {
 };
 // (also zeroes A.peaks[0, n_zero): this pipelined launch's chunk peaks)
 void launch_r2_plan(const MainArgs& A, uint32_t* pieces, int n_zero, int P, hipStream_t s);
+// pipelined batches: the limiter on runs [A.n_runs, A.n_runs_prev) of the
+// previous batch's plan (partners no run of this launch has), one wave each
+void launch_prev_runs(const MainArgs& A, int N, hipStream_t s);
 // k_gate_carry over every run of A (A.run_base = 0): carry-in state id and leaf
 // window per run; H_max frames of look-back before a run is left unresolved
 // gtf (optional): per-run transfer tables [n_runs][gate_D + 2] for chained

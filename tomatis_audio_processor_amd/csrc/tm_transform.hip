@@ -124,7 +124,8 @@ __device__ void limit_own(const MainArgs& A, const TomatisStream& S, int gc, int
                         __HIP_MEMORY_SCOPE_AGENT)));
   if (!(peak > A.limit)) return;
   const float sc = A.limit / peak;
-  const int64_t a = max(lo, A.chunk_rng[2 * gc]), b = min(hi, A.chunk_rng[2 * gc + 1]);
+  const int64_t* const rng = prev ? A.chunk_rng_prev : A.chunk_rng;
+  const int64_t a = max(lo, rng[2 * gc]), b = min(hi, rng[2 * gc + 1]);
   if (b <= a) return;
   float* base = (prev ? A.yprev : A.y) + S.out_off + a * CH;
   int64_t n = (b - a) * CH;
@@ -148,6 +149,34 @@ __device__ void limit_own(const MainArgs& A, const TomatisStream& S, int gc, int
   }
   const int64_t t0 = n4 << 2;
   if (t0 + lane < n) base[t0 + lane] = base[t0 + lane] * sc;
+}
+
+// Pipelined batches: the limiter over partner run pr's output (the previous
+// batch's plan, A.runs_prev / A.st_prev) except its blocks [p_lead, p_done),
+// which the frame loop scaled; output-relative ranges split over the nw waves
+// of the sequence (this is wave w)
+template <int CH>
+__device__ void partner_tail(const MainArgs& A, int pr, int HOP, int N, int p_lead, int p_done,
+                             int nw, int w, int lane) {
+  const Run RP = A.runs_prev[pr];
+  const TomatisStream SP = A.st_prev[RP.s];
+  const int64_t s_kaP = SP.first_start + RP.ka * HOP;
+  const int64_t s_lastP = SP.first_start + (RP.kb - 1) * HOP;
+  const int64_t endP = SP.out_begin + SP.out_len;
+  auto tail = [&](int64_t lo, int64_t hi) {  // output-relative [lo, hi)
+    if (lo >= hi) return;
+    const int64_t span = hi - lo, per = (span + nw - 1) / nw;
+    const int64_t wlo = lo + per * w, whi = min(hi, wlo + per);
+    const int c0 = chunk_of(lo + SP.out_begin, SP), c1 = chunk_of(hi - 1 + SP.out_begin, SP);
+    for (int c = c0; c <= c1; ++c) {
+      if (((A.edge_mask & 1) && c == 0) || ((A.edge_mask & 2) && c == SP.n_chunks - 1)) continue;
+      limit_own<CH>(A, SP, SP.chunk_base + c, wlo, whi, lane, true);
+    }
+  };
+  const int64_t hi = min(s_lastP + ((RP.last & 1) ? (int64_t)N : (int64_t)HOP), endP) - SP.out_begin;
+  if (p_lead > 0)  // the leading partial blocks
+    tail(max(s_kaP, SP.out_begin) - SP.out_begin, min(s_kaP + (int64_t)p_lead * HOP - SP.out_begin, hi));
+  tail(max(s_kaP + (int64_t)max(p_done, p_lead) * HOP, SP.out_begin) - SP.out_begin, hi);
 }
 
 template <int CH>
@@ -636,9 +665,9 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       const int pr = run_id;
       plist = (cu32*)(A.pieces) + (int64_t)run_loc * 2 * (A.max_pieces + 1);
       np = (int)plist[0];
-      if (np > 0) {
-        const Run RP = A.runs[pr];
-        const TomatisStream SP = A.st[RP.s];
+      if (np > 0) {  // (k_r2_plan lists pieces only for partners pr < n_runs_prev)
+        const Run RP = A.runs_prev[pr];
+        const TomatisStream SP = A.st_prev[RP.s];
         const int64_t off = SP.out_off + CH * (SP.first_start + RP.ka * HOP - SP.out_begin);
         const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)off);
         const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)off >> 32));
@@ -972,32 +1001,10 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       limit_own<CH>(A, S, S.chunk_base + c, wlo, whi, L & 63);
     }
   }
-  if constexpr (PR) {  // the partner's output not scaled in the frame loop
-    const bool prev = true;  // the previous batch: final, no waits
+  if constexpr (PR) {  // the partner's output not scaled in the frame loop (final, no waits)
     const int pr = valid ? run_id : -1;
-    if (pr >= 0 && A.limit > 0.f) {
-      const Run RP = A.runs[pr];
-      const TomatisStream SP = A.st[RP.s];
-      const int64_t s_kaP = SP.first_start + RP.ka * HOP;
-      const int64_t s_lastP = SP.first_start + (RP.kb - 1) * HOP;
-      const int64_t endP = SP.out_begin + SP.out_len;
-      auto tail = [&](int64_t lo, int64_t hi) {  // output-relative [lo, hi)
-        if (lo >= hi) return;
-        const int nw = P / 64, w = L >> 6;
-        const int64_t span = hi - lo, per = (span + nw - 1) / nw;
-        const int64_t wlo = lo + per * w, whi = min(hi, wlo + per);
-        const int c0 = chunk_of(lo + SP.out_begin, SP), c1 = chunk_of(hi - 1 + SP.out_begin, SP);
-        for (int c = c0; c <= c1; ++c) {
-          if (((A.edge_mask & 1) && c == 0) || ((A.edge_mask & 2) && c == SP.n_chunks - 1)) continue;
-          limit_own<CH>(A, SP, SP.chunk_base + c, wlo, whi, L & 63, prev);
-        }
-      };
-      const int64_t hi = min(s_lastP + ((RP.last & 1) ? (int64_t)N : (int64_t)HOP), endP) - SP.out_begin;
-      if (p_lead > 0)  // the leading partial blocks
-        tail(max(s_kaP, SP.out_begin) - SP.out_begin,
-             min(s_kaP + (int64_t)p_lead * HOP - SP.out_begin, hi));
-      tail(max(s_kaP + (int64_t)max(p_done, p_lead) * HOP, SP.out_begin) - SP.out_begin, hi);
-    }
+    if (pr >= 0 && pr < A.n_runs_prev && A.limit > 0.f)
+      partner_tail<CH>(A, pr, HOP, N, p_lead, p_done, P / 64, L >> 6, L & 63);
   }
 #ifdef TM_PROFILE
   if (valid && (R.last & kRunInterior) && L == 0) {
@@ -1027,11 +1034,12 @@ __global__ __launch_bounds__(64) void k_r2_plan(MainArgs A, uint32_t* __restrict
   if (t >= A.n_runs) return;
   uint32_t* o = out + (int64_t)t * 2 * (A.max_pieces + 1);
   const int run = A.run_base + t;
-  const int pr = run;  // the same run of the previous batch
+  const int pr = run;  // the same run of the previous batch (its plan's runs)
   int n = 0, stop = 0, lead = 0;
-  if (pr >= 0 && (any_run || ((A.runs[pr].last & kRunInterior) && (A.runs[run].last & kRunInterior)))) {
-    const Run R = A.runs[run], RP = A.runs[pr];
-    const TomatisStream SP = A.st[RP.s];
+  if (pr >= 0 && pr < A.n_runs_prev &&
+      (any_run || ((A.runs_prev[pr].last & kRunInterior) && (A.runs[run].last & kRunInterior)))) {
+    const Run R = A.runs[run], RP = A.runs_prev[pr];
+    const TomatisStream SP = A.st_prev[RP.s];
     const int hop = A.hop;
     const int nit = (int)(R.kb - max<int64_t>(0, R.ka - (A.rmax - 1)));
     const int cap = min(nit, A.max_pieces);
@@ -1086,6 +1094,16 @@ __global__ __launch_bounds__(64) void k_r2_plan(MainArgs A, uint32_t* __restrict
     o[0] = (uint32_t)n;
     o[1] = (uint32_t)stop | ((uint32_t)lead << 24);
   }
+}
+
+// Pipelined batches whose previous batch's plan has more runs than this one:
+// partner runs [n_runs, n_runs_prev) get the limiter here (one wave each, no
+// piece list: the whole run, as a transform's tail does)
+template <int CH>
+__global__ __launch_bounds__(64) void k_prev_runs(MainArgs A, int N) {
+  const int pr = A.n_runs + blockIdx.x;
+  if (pr >= A.n_runs_prev || !(A.limit > 0.f)) return;
+  partner_tail<CH>(A, pr, A.hop, N, 0, 0, 1, 0, threadIdx.x);
 }
 
 // In-kernel gate, part 1 (tomatis_stft_ola_gated): per run, the gate state
@@ -1847,6 +1865,13 @@ void launch_r2_plan(const MainArgs& A, uint32_t* pieces, int n_zero, int P, hipS
     return;
   }
   hipLaunchKernelGGL(k_r2_plan, dim3(A.n_runs), dim3(64), 0, s, A, pieces, n_zero, P > 64 ? 1 : 0);
+}
+
+void launch_prev_runs(const MainArgs& A, int N, hipStream_t s) {
+  const int n = A.n_runs_prev - A.n_runs;
+  if (n <= 0 || !A.yprev) return;
+  if (A.ch == 2) hipLaunchKernelGGL(k_prev_runs<2>, dim3(n), dim3(64), 0, s, A, N);
+  else hipLaunchKernelGGL(k_prev_runs<1>, dim3(n), dim3(64), 0, s, A, N);
 }
 
 void launch_gate_carry(const MainArgs& A, int P, int SH, int ch, int32_t* gcarry, float* gwin,

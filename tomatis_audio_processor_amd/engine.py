@@ -387,7 +387,7 @@ class GatePipeline:
                  fc=1000.0, slope=12.0, c1_low=15.0, c1_high=-15.0, c2_low=-15.0,
                  c2_high=15.0, up_delay_ms=250.0, n_fft=4096, hop=2048,
                  output_gain_db=0.0, xfade_ms=None, geometry=None, fused_levels=True,
-                 pipelined=False):
+                 pipelined=False, second_buffer=True):
         """``geometry``: optional per-stream dicts (first_start, n_frames,
         out_begin, out_len, chunk_first, chunk_len, n_chunks) replacing the
         reference schedule -- a time shard of a longer stream (timeshard.py).
@@ -401,7 +401,12 @@ class GatePipeline:
         (two output buffers, alternating), so the limiter's HBM re-read overlaps
         compute instead of ending every pass.  A pass's output is final after
         the next run() or flush(); result() flushes.  Same results bit for bit.
-        Shapes the pipelined calls decline run unpipelined."""
+        Shapes the pipelined calls decline run unpipelined.  The previous pass
+        may also be ANOTHER pipeline's (a multi-file job whose batches differ:
+        ``run(prev_pipe=...)``, the *_pipelined_after calls).
+        ``second_buffer``: allocate the alternate output buffer up front (the
+        default) or only when a second pass of this pipeline needs it (one pass
+        per pipeline, as batch.py runs them: no idle 1x output of HBM)."""
         torch = _torch()
         _check_fft(n_fft, hop, ss.ch)
         self.ss, self.n_fft, self.hop = ss, n_fft, hop
@@ -482,33 +487,79 @@ class GatePipeline:
         self.gate_fallbacks = 0   # gated passes re-run on the two-pass chain
         self.pipelined = bool(pipelined)
         self.pending = False      # pipelined: self.y awaits its limiter
+        self._after = None        # run(prev_pipe=...): another pipeline's pending pass
         if self.pipelined:
-            self._ys = [self.y, torch.empty_like(self.y)]
-            self._pks = [self.peaks, torch.zeros_like(self.peaks)]
+            self._ys = [self.y, torch.empty_like(self.y) if second_buffer else None]
+            self._pks = [self.peaks, torch.zeros_like(self.peaks) if second_buffer else None]
             self._cur = 0
 
-    def run(self, marks=None, check_device: bool = True):
+    def run(self, marks=None, check_device: bool = True, prev_pipe=None):
         """Launch the whole chain on the current stream.
 
         ``marks``: optional pair of torch.cuda.Event recorded on this stream
         around the fused STFT-OLA launch (bench.py's live kernel timing).
         ``check_device``: read the plan's device error word before returning
         (one host synchronisation; ``finish_plan``).  Only a caller that checks
-        once after many passes (bench.py's timed loop) turns it off."""
-        if self.fused_levels:
-            self.gated_used = self._gated(marks)
-            if self.gated_used:
-                if marks:
-                    marks[1].record()
-                if check_device:
-                    self.finish()
-                # pipelined: the output is final after the next pass or flush()
-                return None if self.pending else self.result()
-            self.fused_levels = False  # declined: this plan's shape runs two passes
-        self._two_pass(marks)
+        once after many passes (bench.py's timed loop) turns it off.
+        ``prev_pipe``: another pipeline (same n_fft / hop / channels) whose last
+        pass is pending: this pass limits it inside its transform (pipelined
+        mode), or it is flushed here; either way its output is final once this
+        pass's work on the stream has completed."""
+        if prev_pipe is not None and prev_pipe.pending and self.pending:
+            self.flush()          # one predecessor per pass: ours is limited now
+        self._after = prev_pipe if (prev_pipe is not None and prev_pipe.pending) else None
+        try:
+            if self.fused_levels:
+                self.gated_used = self._gated(marks)
+                if self.gated_used:
+                    if marks:
+                        marks[1].record()
+                    self._flush_after()
+                    if check_device:
+                        self.finish()
+                    # pipelined: the output is final after the next pass or flush()
+                    return None if self.pending else self.result()
+                self.fused_levels = False  # declined: this plan's shape runs two passes
+            self._two_pass(marks)
+            self._flush_after()
+        finally:
+            self._after = None
         if check_device:
             self.finish()
         return None if self.pending else self.result()
+
+    def _prev(self):
+        """(plan, y, peaks) of the output this pass limits: another
+        pipeline's pending pass (run(prev_pipe=...)), this pipeline's own, or
+        none."""
+        a = self._after
+        if a is not None and a.pending:
+            return a.plan, a.y, a.peaks
+        if self.pending:
+            return self.plan, self._ys[self._cur], self._pks[self._cur]
+        return None, None, None
+
+    def _out_slot(self) -> int:
+        """The output buffer of a pipelined pass: the other one while this
+        pipeline's own previous pass is pending, else the current one."""
+        nxt = (1 - self._cur) if self.pending else self._cur
+        if self._ys[nxt] is None:   # second_buffer=False: allocated on first need
+            self._ys[nxt] = _torch().empty_like(self._ys[self._cur])
+            self._pks[nxt] = _torch().zeros_like(self._pks[self._cur])
+        return nxt
+
+    def _took_prev(self, nxt: int):
+        """Bookkeeping after a pipelined launch into buffer ``nxt``."""
+        if self._after is not None:
+            self._after.pending = False   # limited inside that launch
+        self._cur = nxt
+        self.y, self.peaks = self._ys[nxt], self._pks[nxt]
+        self.pending = True
+
+    def _flush_after(self):
+        a = self._after
+        if a is not None and a.pending:
+            a.flush()
 
     def _gated(self, marks=None) -> bool:
         """levels + gate + transform + limiter in one pass over the input (the
@@ -532,26 +583,24 @@ class GatePipeline:
         return True
 
     def _pipelined_pass(self, marks=None) -> bool:
-        """One pipelined pass into the other output buffer, limiting the
-        pending one inside the launch; False (nothing launched) when the
-        library declines the shape (then pipelining stays off)."""
+        """One pipelined pass, limiting the pending output (this pipeline's
+        previous pass, or run(prev_pipe=...)'s) inside the launch; False (nothing
+        launched) when the library declines the shape (then pipelining stays
+        off)."""
         L, hs = lib(), stream_handle()
-        nxt = 1 - self._cur
-        prev_y = self._ys[self._cur] if self.pending else None
-        prev_pk = self._pks[self._cur] if self.pending else None
+        nxt = self._out_slot()
+        pplan, prev_y, prev_pk = self._prev()
         if marks:  # (the call zeroes this pass's chunk peaks itself)
             marks[0].record()
-        rc = L.tomatis_stft_ola_gated_pipelined(
+        rc = L.tomatis_stft_ola_gated_pipelined_after(
             self.plan.h, ptr(self.ss.x), ptr(self.gains), self.n_rows, ptr(self._ys[nxt]),
-            ptr(self._pks[nxt]), PEAK_LIMIT, ptr(self.r), ptr(self.states), ptr(prev_y),
-            ptr(prev_pk), hs)
+            ptr(self._pks[nxt]), PEAK_LIMIT, ptr(self.r), ptr(self.states),
+            pplan.h if pplan is not None else None, ptr(prev_y), ptr(prev_pk), hs)
         if rc == E_UNSUPPORTED:
             self.pipelined = False
             return False
         check(rc, "stft_ola_gated_pipelined")
-        self._cur = nxt
-        self.y, self.peaks = self._ys[nxt], self._pks[nxt]
-        self.pending = True
+        self._took_prev(nxt)
         return True
 
     def flush(self):
@@ -578,20 +627,17 @@ class GatePipeline:
     def _rows_pipelined_pass(self) -> bool:
         """The two-pass chain's transform as a pipelined pass (gain-row ids from
         tomatis_gate_std); False (nothing launched) when the library declines."""
-        nxt = 1 - self._cur
-        prev_y = self._ys[self._cur] if self.pending else None
-        prev_pk = self._pks[self._cur] if self.pending else None
-        rc = lib().tomatis_stft_ola_pipelined(  # (zeroes this pass's chunk peaks)
+        nxt = self._out_slot()
+        pplan, prev_y, prev_pk = self._prev()
+        rc = lib().tomatis_stft_ola_pipelined_after(  # (zeroes this pass's chunk peaks)
             self.plan.h, ptr(self.ss.x), ptr(self.gains), self.n_rows, ptr(self.rows),
-            ptr(self._ys[nxt]), ptr(self._pks[nxt]), PEAK_LIMIT, ptr(prev_y), ptr(prev_pk),
-            stream_handle())
+            ptr(self._ys[nxt]), ptr(self._pks[nxt]), PEAK_LIMIT,
+            pplan.h if pplan is not None else None, ptr(prev_y), ptr(prev_pk), stream_handle())
         if rc == E_UNSUPPORTED:
             self.pipelined = False
             return False
         check(rc, "stft_ola_pipelined")
-        self._cur = nxt
-        self.y, self.peaks = self._ys[nxt], self._pks[nxt]
-        self.pending = True
+        self._took_prev(nxt)
         return True
 
     def _limited(self):
@@ -728,15 +774,16 @@ class AdaptivePipeline:
         self.out_offs = out_offs
         self.pipelined = bool(pipelined)
         self.pending = False      # pipelined: self.y awaits its limiter
+        self._after = None        # run(prev_pipe=...): another pipeline's pending pass
         if self.pipelined:
             self._ys = [self.y, out2 if out2 is not None else torch.empty_like(self.y)]
             self._pks = [self.peaks, torch.zeros_like(self.peaks)]
             self._cur = 0
 
-    def run(self, marks=None, timer=None, check_device: bool = True):
+    def run(self, marks=None, timer=None, check_device: bool = True, prev_pipe=None):
         """``timer`` (a dict) collects synchronised wall-clock phases (profiling).
-        ``check_device``: as GatePipeline.run."""
-        for _ in self.steps(marks, timer):
+        ``check_device``, ``prev_pipe``: as GatePipeline.run."""
+        for _ in self.steps(marks, timer, prev_pipe=prev_pipe):
             pass
         if check_device:
             self.finish()
@@ -746,10 +793,18 @@ class AdaptivePipeline:
         """STFT-gain-OLA, normalise max(w,1e-8), restore, global limiter (one
         chunk per stream: fused into the transform when its runs allow;
         pipelined: the previous pass's limiter inside this transform)"""
-        if self.pipelined and self._pipelined_pass():
-            return
-        self.flush()
-        self._limited()
+        a = self._after
+        if a is not None and a.pending and self.pending:
+            self.flush()          # one predecessor per pass
+        try:
+            if self.pipelined and self._pipelined_pass():
+                return
+            self.flush()
+            self._limited()
+        finally:
+            if a is not None and a.pending:
+                a.flush()
+            self._after = None
 
     def _limited(self):
         self.peaks.zero_()
@@ -759,17 +814,24 @@ class AdaptivePipeline:
               "stft_ola_limited")
 
     def _pipelined_pass(self) -> bool:
-        nxt = 1 - self._cur
-        prev_y = self._ys[self._cur] if self.pending else None
-        prev_pk = self._pks[self._cur] if self.pending else None
-        rc = lib().tomatis_stft_ola_pipelined(  # (zeroes this pass's chunk peaks)
+        a = self._after
+        nxt = 1 - self._cur   # (AdaptiveGroups: every group alternates in step)
+        if a is not None and a.pending:
+            pplan, prev_y, prev_pk = a.plan, a.y, a.peaks
+        elif self.pending:
+            pplan, prev_y, prev_pk = self.plan, self._ys[self._cur], self._pks[self._cur]
+        else:
+            pplan, prev_y, prev_pk = None, None, None
+        rc = lib().tomatis_stft_ola_pipelined_after(  # (zeroes this pass's chunk peaks)
             self.plan.h, ptr(self.ss.x), ptr(self.gains), self.n_rows, ptr(self.rows),
-            ptr(self._ys[nxt]), ptr(self._pks[nxt]), PEAK_LIMIT, ptr(prev_y), ptr(prev_pk),
-            stream_handle())
+            ptr(self._ys[nxt]), ptr(self._pks[nxt]), PEAK_LIMIT,
+            pplan.h if pplan is not None else None, ptr(prev_y), ptr(prev_pk), stream_handle())
         if rc == E_UNSUPPORTED:
             self.pipelined = False
             return False
         check(rc, "stft_ola_pipelined")
+        if a is not None:
+            a.pending = False     # limited inside this launch
         self._cur = nxt
         self.y, self.peaks = self._ys[nxt], self._pks[nxt]
         self.pending = True
@@ -795,12 +857,13 @@ class AdaptivePipeline:
         with torch.cuda.stream(self.stream or torch.cuda.current_stream()):
             return finish_plan(self.plan, redo, "AdaptivePipeline")
 
-    def steps(self, marks=None, timer=None, after=None):
+    def steps(self, marks=None, timer=None, after=None, prev_pipe=None):
         """The pass as a generator that yields wherever the host would wait for
         the device (the input peaks, the frame r) and before the transform, so a
         driver can interleave several pipelines on their own streams
         (AdaptiveGroups).  ``after``: a callable giving an event (or a list of
-        events) the transform waits for."""
+        events) the transform waits for.  ``prev_pipe``: as GatePipeline.run
+        (the caller orders that pipeline's stream before this one's)."""
         torch = _torch()
         strm = self.stream or torch.cuda.current_stream()
         L, P = lib(), self.plan.h
@@ -924,6 +987,7 @@ class AdaptivePipeline:
                         strm.wait_event(e)
             if marks and marks[0] is not None:
                 marks[0].record()
+            self._after = prev_pipe if (prev_pipe is not None and prev_pipe.pending) else None
             self._transform()
             if marks and marks[1] is not None:
                 marks[1].record()
@@ -1024,9 +1088,19 @@ class AdaptiveGroups:
             self.pipes.append(p)
         self.ss = ss
 
-    def run(self, marks=None, check_device: bool = True):
+    def run(self, marks=None, check_device: bool = True, prev_pipe=None):
+        """``prev_pipe``: another AdaptiveGroups (or AdaptivePipeline) whose
+        last pass is pending: group g limits its group g inside its transform
+        (groups it does not have are flushed)."""
         torch = _torch()
         cur = torch.cuda.current_stream()
+        prevs = []
+        if prev_pipe is not None:
+            prevs = list(getattr(prev_pipe, "pipes", [prev_pipe]))
+            for q in prevs[len(self.pipes):]:
+                q.flush()
+            for q in prevs:   # (their last transforms are ordered before cur)
+                cur.wait_stream(q.stream or cur)
         for p in self.pipes:
             p.stream.wait_stream(cur)
         G = len(self.pipes)
@@ -1047,7 +1121,7 @@ class AdaptiveGroups:
                 after = (lambda: [q.prep_done for q in self.pipes[1:]])
             else:
                 after = None
-            gens.append(p.steps(mk, after=after))
+            gens.append(p.steps(mk, after=after, prev_pipe=prevs[g] if g < len(prevs) else None))
         live = list(gens)
         while live:
             for gen in list(live):
@@ -1057,9 +1131,30 @@ class AdaptiveGroups:
                     live.remove(gen)
         for p in self.pipes:
             cur.wait_stream(p.stream)
+        self._lockstep()
         if check_device:
             self.finish()
         return None if self.pending else self.result()
+
+    def _lockstep(self):
+        """Pipelining is decided for all groups at once: if any
+        group's pass declined it, every group flushes and stops pipelining, and
+        outputs left in the other buffer move into the first group's."""
+        if all(p.pipelined for p in self.pipes) or not any(p.pipelined for p in self.pipes):
+            return
+        torch = _torch()
+        cur = torch.cuda.current_stream()
+        for p in self.pipes:
+            p.flush()
+            cur.wait_stream(p.stream)
+            p.pipelined = False
+        y0 = self.pipes[0].y
+        for p in self.pipes[1:]:
+            if p.y.data_ptr() != y0.data_ptr():
+                for o, n in zip(p.out_offs, [s.out_len for s in list(p.plan.streams)[:p.ss.n_streams]]):
+                    y0[o:o + n * p.ss.ch].copy_(p.y[o:o + n * p.ss.ch])
+                p.y = y0
+        self.y = y0
 
     @property
     def pending(self) -> bool:
@@ -1077,6 +1172,7 @@ class AdaptiveGroups:
         for p in self.pipes:
             p.flush()
             cur.wait_stream(p.stream)
+        self.y = self.pipes[0].y
 
     def finish(self) -> int:
         bits = 0
