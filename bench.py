@@ -481,7 +481,7 @@ def main():
     # distinct files (pass k+1 limits pass k inside its transform), as batch.py
     # runs a multi-file job
     one = None
-    if a.single_steps > 0 and not strong and not a.no_pipeline:
+    if a.single_steps > 0 and mode != "timeshard" and not a.no_pipeline:
         p1 = make_pipe(False)
         for w in range(2):
             set_input(p1, w)

@@ -73,7 +73,7 @@ def _result_of(E, pipe, y, peaks, r, states, alpha):
                     alpha=alpha, chunk_peaks=peaks, chunk_base=[s.chunk_base for s in st],
                     n_chunks=[s.n_chunks for s in st],
                     extra=dict(bounds=pipe.bounds, n_fft=pipe.n_fft, norm="eps", limit=LIM,
-                               out_begin=[s.out_begin for s in st]))
+                               limiter_applied=True, out_begin=[s.out_begin for s in st]))
 
 
 def _gate_passes(torch, E, ss, xs, kw, check_mid):

@@ -1547,22 +1547,13 @@ __global__ __launch_bounds__(256) void k_scale_copy(const float* __restrict__ x,
 }
 
 // HBM bandwidth probe (bench.py's roofline.achievable_peak):
-// y = x as 16-byte streaming loads / stores, 4 in flight per lane
+// y = x, one 16-byte load and store per thread, one 256-thread block per 4 KB
+// (tools/copy_probe.hip: 6.2 TB/s on MI355X, the fastest of the grid-stride,
+// unrolled, streaming-hint and per-block-chunk forms measured)
 __global__ __launch_bounds__(256) void k_copy_probe(const float4* __restrict__ x,
                                                     float4* __restrict__ y, int64_t n4) {
-  typedef float f4v __attribute__((ext_vector_type(4)));
-  const f4v* xv = reinterpret_cast<const f4v*>(x);
-  f4v* yv = reinterpret_cast<f4v*>(y);
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (; i + 3 * stride < n4; i += 4 * stride) {
-    f4v t[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) t[u] = __builtin_nontemporal_load(xv + i + u * stride);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) __builtin_nontemporal_store(t[u], yv + i + u * stride);
-  }
-  for (; i < n4; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(xv + i), yv + i);
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n4) y[i] = x[i];
 }
 
 // PCM <-> float at the file boundary, libsndfile's
@@ -3165,11 +3156,8 @@ int tomatis_copy_probe(const float* x, float* y, int64_t n, void* hs) {
     return TOMATIS_E_ARG;
   const int64_t n4 = n / 4;
   if (n4 == 0) return TOMATIS_OK;
-  int dev = 0, ncu = 256;
-  if (hipGetDevice(&dev) == hipSuccess)
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  // 8 blocks per CU, each lane 4 x 16 bytes per trip
-  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((int64_t)ncu * 8, (n4 + 1023) / 1024));
+  if (n4 > (int64_t)0x7fffffff * 256) return TOMATIS_E_ARG;
+  const unsigned g = (unsigned)((n4 + 255) / 256);
   hipLaunchKernelGGL(k_copy_probe, dim3(g), dim3(256), 0, (hipStream_t)hs,
                      reinterpret_cast<const float4*>(x), reinterpret_cast<float4*>(y), n4);
   return launch_check();

@@ -596,6 +596,8 @@ class GatePipeline:
             self.plan.h, ptr(self.ss.x), ptr(self.gains), self.n_rows, ptr(self._ys[nxt]),
             ptr(self._pks[nxt]), PEAK_LIMIT, ptr(self.r), ptr(self.states),
             pplan.h if pplan is not None else None, ptr(prev_y), ptr(prev_pk), hs)
+        if rc == E_UNSUPPORTED and self._drop_foreign_prev(pplan):
+            return self._pipelined_pass(marks)  # (marks[0] recorded again: same point)
         if rc == E_UNSUPPORTED:
             self.pipelined = False
             return False
@@ -633,11 +635,25 @@ class GatePipeline:
             self.plan.h, ptr(self.ss.x), ptr(self.gains), self.n_rows, ptr(self.rows),
             ptr(self._ys[nxt]), ptr(self._pks[nxt]), PEAK_LIMIT,
             pplan.h if pplan is not None else None, ptr(prev_y), ptr(prev_pk), stream_handle())
+        if rc == E_UNSUPPORTED and self._drop_foreign_prev(pplan):
+            return self._rows_pipelined_pass()
         if rc == E_UNSUPPORTED:
             self.pipelined = False
             return False
         check(rc, "stft_ola_pipelined")
         self._took_prev(nxt)
+        return True
+
+    def _drop_foreign_prev(self, pplan) -> bool:
+        """A pipelined call declined another pipeline's pending pass (a plan of
+        another n_fft / hop / channel count): flush that one on its own plan and
+        let the caller retry with nothing to limit.  False when the decline is
+        this plan's own shape."""
+        a = self._after
+        if a is None or pplan is None or pplan is self.plan:
+            return False
+        a.flush()
+        self._after = None
         return True
 
     def _limited(self):
@@ -826,6 +842,10 @@ class AdaptivePipeline:
             self.plan.h, ptr(self.ss.x), ptr(self.gains), self.n_rows, ptr(self.rows),
             ptr(self._ys[nxt]), ptr(self._pks[nxt]), PEAK_LIMIT,
             pplan.h if pplan is not None else None, ptr(prev_y), ptr(prev_pk), stream_handle())
+        if rc == E_UNSUPPORTED and a is not None and pplan is a.plan:
+            a.flush()             # another shape: limited on its own plan, then retry
+            self._after = None
+            return self._pipelined_pass()
         if rc == E_UNSUPPORTED:
             self.pipelined = False
             return False
