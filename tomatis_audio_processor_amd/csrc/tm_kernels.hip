@@ -1696,7 +1696,6 @@ struct tomatis_plan_s {
   int xs_max_pieces = 0;
   // in-kernel levels + gate (tomatis_stft_ola_gated): per-run carry-in
   int32_t* gate_carry = nullptr;
-  float* gate_win = nullptr;
   int gate_cap = 0;
   uint16_t* gate_tf = nullptr;     // chained runs' transfer tables [gate_cap][D + 2]
   // the look-back the carries in gate_carry belong to (input, run layout)
@@ -1790,7 +1789,7 @@ int tomatis_plan_destroy(tomatis_plan_t p) {
                   p->grp_base, p->leaf_base, p->leaves, p->gsum, p->gcarry, p->gcarry_in,
                   p->aq, p->afin, p->acin,
                   p->chunk_need, p->chunk_done, p->chunk_rng, p->err, p->twL,
-                  p->xs_pieces, p->gate_carry, p->gate_win,
+                  p->xs_pieces, p->gate_carry,
                   p->gate_tf,
                   p->pw_leaf, p->pw_prog, p->blue_b, p->blue_h, p->glb_work};
   for (void* q : ptrs) dfree(q);
@@ -2639,20 +2638,17 @@ struct GateOut {
   bool lookback_done;  // tomatis_gate_lookback ran for this input on this stream
 };
 
-// per-run carry-in state id and leaf window of the fused gate (k_gate_carry)
+// per-run carry-in state id of the fused gate (k_gate_carry)
 static int gate_lookback(tomatis_plan_s* p, const float* x, hipStream_t s) {
   const int nst = p->d.up_delay_frames + 2;
   const bool chain = nst <= kGateChainStates;
   if (p->n_runs > p->gate_cap) {
     dfree(p->gate_carry);
-    dfree(p->gate_win);
     dfree(p->gate_tf);
     p->gate_carry = nullptr;
-    p->gate_win = nullptr;
     p->gate_tf = nullptr;
     p->gate_cap = 0;
-    if (hipMalloc(reinterpret_cast<void**>(&p->gate_carry), (size_t)p->n_runs * sizeof(int32_t)) ||
-        hipMalloc(reinterpret_cast<void**>(&p->gate_win), (size_t)p->n_runs * 16 * sizeof(float)))
+    if (hipMalloc(reinterpret_cast<void**>(&p->gate_carry), (size_t)p->n_runs * sizeof(int32_t)))
       return TOMATIS_E_NOMEM;
     if (chain && hipMalloc(reinterpret_cast<void**>(&p->gate_tf),
                            (size_t)p->n_runs * nst * sizeof(uint16_t)))
@@ -2671,8 +2667,7 @@ static int gate_lookback(tomatis_plan_s* p, const float* x, hipStream_t s) {
   A.hop = p->d.hop;
   A.ch = p->d.ch;
   A.gate_D = p->d.up_delay_frames;
-  launch_gate_carry(A, p->P, p->SH, p->d.ch, p->gate_carry, p->gate_win,
-                    chain ? p->gate_tf : nullptr, s);
+  launch_gate_carry(A, p->P, p->SH, p->d.ch, p->gate_carry, chain ? p->gate_tf : nullptr, s);
   return launch_check();
 }
 
@@ -2807,7 +2802,7 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
   A.r_out = nullptr;
   A.st_out = nullptr;
   A.gcarry = nullptr;
-  A.gwin = nullptr;
+  A.gtf = nullptr;
   A.yprev = nullptr;
   A.peaks_prev = nullptr;
   A.runs_prev = p->runs;
@@ -2827,7 +2822,7 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
     A.r_out = gate->r;
     A.st_out = gate->states;
     A.gcarry = p->gate_carry;
-    A.gwin = p->gate_win;
+    A.gtf = (p->d.up_delay_frames + 2 <= kGateChainStates) ? p->gate_tf : nullptr;
   }
   if (limit > 0.f) {
     if (!p->chunk_done) return TOMATIS_E_UNSUPPORTED;

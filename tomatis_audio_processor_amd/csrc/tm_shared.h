@@ -93,19 +93,21 @@ struct MainArgs {
   int gate_D;           // up-delay frames
   float* r_out;
   uint8_t* st_out;
-  const int32_t* gcarry;  // per run: state id before its first frame (< 0: unresolved)
-  const float* gwin;      // per run: the 16 leaf sums of the frame before its first
+  const int32_t* gcarry;  // per run: state id before its first frame (< 0: unresolved,
+                          // kGateChained: compose gtf from the nearest resolved run)
+  const uint16_t* gtf;    // chained runs' transfer tables [run][gate_D + 2]
 };
 // (also zeroes A.peaks[0, n_zero): this pipelined launch's chunk peaks)
 void launch_r2_plan(const MainArgs& A, uint32_t* pieces, int n_zero, int P, hipStream_t s);
 // pipelined batches: the limiter on runs [A.n_runs, A.n_runs_prev) of the
 // previous batch's plan (partners no run of this launch has), one wave each
 void launch_prev_runs(const MainArgs& A, int N, hipStream_t s);
-// k_gate_carry over every run of A (A.run_base = 0): carry-in state id and leaf
-// window per run; H_max frames of look-back before a run is left unresolved
+// k_gate_carry over every run of A (A.run_base = 0): carry-in state id per
+// run; kGateLookback frames of look-back (kGateLookbackMax back to the
+// previous run's start when gtf is given) before a run is left unresolved.
 // gtf (optional): per-run transfer tables [n_runs][gate_D + 2] for chained
-// runs, composed by k_gate_chain (one thread per run)
-void launch_gate_carry(const MainArgs& A, int P, int SH, int ch, int32_t* gcarry, float* gwin,
+// runs, composed in the transform's prologue (gate_chain_carry)
+void launch_gate_carry(const MainArgs& A, int P, int SH, int ch, int32_t* gcarry,
                        uint16_t* gtf, hipStream_t s);
 constexpr int kGateLookback = 512;       // look-back limit of a run that cannot chain
 constexpr int kGateLookbackMax = 4096;   // chained runs: frames back to the previous run's start

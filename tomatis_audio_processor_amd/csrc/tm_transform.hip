@@ -382,6 +382,21 @@ __device__ __forceinline__ float lv_frame_r(float lw) {
 // constant-address-space view makes uniform loads s_load (lgkmcnt-counted)
 typedef __attribute__((address_space(4))) const uint32_t cu32;
 
+// Chained gate carries (k_gate_carry marked run r kGateChained): the transfer
+// tables of the chained runs from the nearest earlier resolved run r0 up to r,
+// applied in run order to carry[r0] (-1, unresolved, stays -1).  A stream's
+// first run never chains (its look-back reaches frame 0), so r0 is in r's own
+// stream.  Wave-uniform; every value was written by the previous launch.
+__device__ int gate_chain_carry(const MainArgs& A, int r) {
+  int r0 = r - 1, c = -1;
+  while (r0 >= 0 && (c = __builtin_amdgcn_readfirstlane(A.gcarry[r0])) == kGateChained) --r0;
+  if (r0 < 0) c = -1;
+  const int nst = A.gate_D + 2;
+  for (int q = r0 + 1; q <= r && c >= 0; ++q)
+    c = __builtin_amdgcn_readfirstlane((int)A.gtf[(int64_t)q * nst + c]);
+  return c;
+}
+
 // Fused framing -> window -> FFT -> gain -> IFFT -> window -> OLA -> normalise.
 // One sequence of P lanes (P/64 waves) processes frames [ka - (rmax-1), kb) of
 // one stream and emits the hop block of every frame >= ka.  Lane L register i
@@ -492,21 +507,33 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   const float oscale = S.out_scale;
   const float iscale = S.in_scale;
 
-  // ---- in-kernel gate: carry-in state and leaf window from k_gate_carry ----
+  // ---- in-kernel gate: carry-in state from k_gate_carry ----
   static_assert(!GT || (P == 64 && NR == 32 && (SH == 4 || SH == 8)),
                 "in-kernel levels: n_fft 2048, hop 256 / 512");
   constexpr int NBLK = NR / SH;  // hop blocks per frame
   float lw = 0.f;                // lanes 0..15: the current frame's leaf sums
   int gid = 0;                   // gate state id (tm_gate.h)
   if constexpr (GT) {
-    lw = (L < 16) ? A.gwin[(int64_t)run_id * 16 + L] : 0.f;
     gid = __builtin_amdgcn_readfirstlane(A.gcarry[run_id]);
+    if (gid == kGateChained) gid = gate_chain_carry(A, run_id);
     if (gid < 0) {  // look-back did not resolve: the host re-runs the two-pass path
       if (L == 0) atomicOr(A.err, TOMATIS_ERR_GATE_CARRY);
       gid = 0;
     }
   }
   float* const lscr = reinterpret_cast<float*>(buf);  // leaf scratch (free at the frame top)
+  // the run's first frame: the leaves of its first NBLK - 1 blocks into the
+  // window's last lanes, so the first gate_frame (which appends the newest
+  // block) completes that frame's window (the same leaf code, the same samples)
+  auto start_window = [&](const cf (&fr)[NR]) -> float {
+    float w = 0.f;
+    sfor<0, NBLK - 1>([&](auto bb) {
+      constexpr int B = decltype(bb)::value;
+      w = lv_window<SH, true>(
+          w, lv_leaves<CH, SH, SH * (B + 1)>(*reinterpret_cast<const cf(*)[SH * (B + 1)]>(&fr[0]), lscr, L));
+    });
+    return w;
+  };
   // predicate thresholds in SGPRs; the exception lists (numpy log10's
   // non-monotone steps, rarely non-empty) are read from the stream table only
   // when present, so the frame loop does not hold 10 more SGPRs
@@ -759,6 +786,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       store_out(o, rnull, 0);
       ld_new(min(1, nit - 1), nh);
     }
+    if constexpr (GT) lw = start_window(v);
     for (int it = 0; it < nit; ++it) {
       const bool emit = it >= nwarm;
       uint32_t row;
@@ -920,7 +948,10 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
         for (int u = 0; u < PQ; ++u)
           pbk[u] = __builtin_amdgcn_raw_buffer_load_b128(rpp, L * 16, u * 16 * P, 2);  // (nt)
       }
-      if constexpr (GT) row = gate_frame(v, k, live && k >= R.ka);
+      if constexpr (GT) {
+        if (it == 0) lw = start_window(v);
+        row = gate_frame(v, k, live && k >= R.ka);
+      }
       transform(v, row);
       if constexpr (PV) {
   #pragma unroll
@@ -1107,8 +1138,9 @@ __global__ __launch_bounds__(64) void k_prev_runs(MainArgs A, int N) {
 }
 
 // In-kernel gate, part 1 (tomatis_stft_ola_gated): per run, the gate state
-// before its first frame kf = max(0, ka - rmax + 1) and the 16-leaf window of
-// frame kf - 1, which the fused kernel continues frame by frame.  The gate
+// before its first frame kf = max(0, ka - rmax + 1), from which the fused
+// kernel continues frame by frame (its 16-leaf window it builds from its own
+// first frame's registers).  The gate
 // automaton forgets its past at an anchor frame: a frame that is not "on" and
 // "off" leaves C1 idle whatever came before, and D + 1 consecutive frames "on"
 // and not "off" leave C2 (every pending count matures, C2 stays).  One wave
@@ -1124,13 +1156,12 @@ __global__ __launch_bounds__(64) void k_prev_runs(MainArgs A, int N) {
 // before kf is the state before kc (that run's own carry-in) stepped over the
 // predicates of frames [kc, kf), which the walk has recorded.  The run then
 // stores the automaton's transfer function over those frames (one lane per
-// start state: tf[run][s], s < nst = D + 2) and carry = kGateChained;
-// k_gate_chain composes the carries in run order afterwards.  Only a run whose
+// start state: tf[run][s], s < nst = D + 2) and carry = kGateChained; the
+// transform's prologue composes them (gate_chain_carry).  Only a run whose
 // look-back exceeds kGateLookbackMax frames (or nst > kGateChainStates) stays
 // unresolved (carry -1: the host's two-pass fallback).
 template <int CH, int SH>
 __global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restrict__ carry,
-                                                   float* __restrict__ win,
                                                    uint16_t* __restrict__ tf) {
   constexpr int P = 64, NR = 32, HOP = SH * P, NB = NR / SH, LB = SH / 2, PFD = 4;
   __shared__ __attribute__((aligned(16))) float scr[LB * kLvLS];
@@ -1173,7 +1204,9 @@ __global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restri
     const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e), 48));
     return (r0 + r1) + (r2 + r3);
   };
-  // window of frame kf - 1: blocks kf - 1 .. kf + NB - 2
+  // frame kf - 1 = blocks kf - 1 .. kf + NB - 2: their energies for the fast
+  // walk (the exact leaf window only if the exact walk runs: the transform
+  // builds its own from its first frame's registers)
   float lw = 0.f;
   float eb[NB];  // fast walk: energies of the current frame's blocks, eb[0] the earliest
   {
@@ -1181,12 +1214,8 @@ __global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restri
 #pragma unroll
     for (int i = 0; i < NB; ++i) load_block(kf - 1 + i, b[i]);  // all loads in flight at once
 #pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      eb[i] = block_energy(b[i]);
-      lw = lv_window<SH, true>(lw, lv_leaves<CH, SH, SH>(b[i], scr, L));
-    }
+    for (int i = 0; i < NB; ++i) eb[i] = block_energy(b[i]);
   }
-  if (L < 16) win[(int64_t)run * 16 + L] = lw;
   int id = 0;
   if (kf > 0) {
     int64_t j = kf - 1;          // the window holds frame j
@@ -1251,14 +1280,21 @@ __global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restri
           }
         });
       }
-      if (exact) {  // restart from frame kf - 1
-        j = kf - 1;
-        a_k = -2;
-        a_id = 0;
-        on_run = 0;
-        n = 0;
-        sfor<0, PFD>([&](auto uu) { load_block(j - 1 - decltype(uu)::value, bq[decltype(uu)::value]); });
+    }
+    if (exact) {  // restart from frame kf - 1 on the exact levels (numpy's r)
+      j = kf - 1;
+      a_k = -2;
+      a_id = 0;
+      on_run = 0;
+      n = 0;
+      {
+        cf b[NB][SH];
+#pragma unroll
+        for (int i = 0; i < NB; ++i) load_block(kf - 1 + i, b[i]);
+#pragma unroll
+        for (int i = 0; i < NB; ++i) lw = lv_window<SH, true>(lw, lv_leaves<CH, SH, SH>(b[i], scr, L));
       }
+      sfor<0, PFD>([&](auto uu) { load_block(j - 1 - decltype(uu)::value, bq[decltype(uu)::value]); });
     }
     bool more = exact;
     while (more) {
@@ -1314,30 +1350,6 @@ __global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restri
     }
   }
   if (L == 0) carry[run] = id;
-}
-
-// Chained carries, one thread per run: a chained run's carry is the transfer
-// functions of the chained runs from the nearest earlier non-chained run r0 up
-// to itself, applied in run order to carry[r0] (-1, unresolved, stays -1).  A
-// stream's first run never chains (kc = 0), so r0 is in the run's own stream.
-// Threads finish chained predecessors concurrently: a predecessor read as
-// already composed holds its final carry, which the walk may start from just
-// as well (relaxed 32-bit loads / stores).  Common case (no chained runs): one
-// coalesced load per run.
-__global__ __launch_bounds__(256) void k_gate_chain(int n_runs, int nst,
-                                                    int32_t* __restrict__ carry,
-                                                    const uint16_t* __restrict__ tf) {
-  const int r = blockIdx.x * 256 + threadIdx.x;
-  if (r >= n_runs) return;
-  if (__hip_atomic_load(carry + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != kGateChained)
-    return;
-  int r0 = r - 1, c = -1;
-  while (r0 >= 0 && (c = __hip_atomic_load(carry + r0, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT)) == kGateChained)
-    --r0;
-  if (r0 < 0) c = -1;
-  for (int q = r0 + 1; q <= r && c >= 0; ++q) c = (int)tf[(int64_t)q * nst + c];
-  __hip_atomic_store(carry + r, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Generic hop: same transform, windowed frame outputs to scratch, then a gather.
@@ -1874,22 +1886,17 @@ void launch_prev_runs(const MainArgs& A, int N, hipStream_t s) {
   else hipLaunchKernelGGL(k_prev_runs<1>, dim3(n), dim3(64), 0, s, A, N);
 }
 
-void launch_gate_carry(const MainArgs& A, int P, int SH, int ch, int32_t* gcarry, float* gwin,
+void launch_gate_carry(const MainArgs& A, int P, int SH, int ch, int32_t* gcarry,
                        uint16_t* gtf, hipStream_t s) {
   if (A.n_runs <= 0 || P != 64) return;
   const dim3 g(A.n_runs), b(64);
   if (SH == 8) {
-    if (ch == 2) hipLaunchKernelGGL((k_gate_carry<2, 8>), g, b, 0, s, A, gcarry, gwin, gtf);
-    else hipLaunchKernelGGL((k_gate_carry<1, 8>), g, b, 0, s, A, gcarry, gwin, gtf);
+    if (ch == 2) hipLaunchKernelGGL((k_gate_carry<2, 8>), g, b, 0, s, A, gcarry, gtf);
+    else hipLaunchKernelGGL((k_gate_carry<1, 8>), g, b, 0, s, A, gcarry, gtf);
   } else if (SH == 4) {
-    if (ch == 2) hipLaunchKernelGGL((k_gate_carry<2, 4>), g, b, 0, s, A, gcarry, gwin, gtf);
-    else hipLaunchKernelGGL((k_gate_carry<1, 4>), g, b, 0, s, A, gcarry, gwin, gtf);
-  } else {
-    return;
+    if (ch == 2) hipLaunchKernelGGL((k_gate_carry<2, 4>), g, b, 0, s, A, gcarry, gtf);
+    else hipLaunchKernelGGL((k_gate_carry<1, 4>), g, b, 0, s, A, gcarry, gtf);
   }
-  if (gtf)
-    hipLaunchKernelGGL(k_gate_chain, dim3((A.n_runs + 255) / 256), dim3(256), 0, s, A.n_runs,
-                       A.gate_D + 2, gcarry, gtf);
 }
 
 void launch_lds_gather(const LdsArgs& A, hipStream_t s) {
