@@ -80,6 +80,32 @@ def edge_index(out_len: int, n_fft: int) -> np.ndarray:
     return np.unique(np.concatenate([np.arange(k), np.arange(out_len - k, out_len)]))
 
 
+def _range_max(v: np.ndarray, lo: np.ndarray, hi: np.ndarray) -> np.ndarray:
+    """max(v[lo[t]:hi[t]]) per query t (0 where the range is empty): a sparse
+    table of power-of-two range maxima, two overlapping lookups per query
+    (exact: the same elements' max as a slice per query)."""
+    out = np.zeros(len(lo))
+    ln = hi - lo
+    ok = ln > 0
+    if not ok.any():
+        return out
+    table = [v]
+    k = 1
+    while 2 * k <= len(v):
+        prev = table[-1]
+        table.append(np.maximum(prev[:-k], prev[k:]))  # table[j][i] = max v[i : i + 2^j]
+        k *= 2
+    idx = np.nonzero(ok)[0]
+    j = np.floor(np.log2(ln[idx])).astype(np.int64)
+    j = np.where((1 << (j + 1)) <= ln[idx], j + 1, j)  # guard log2 rounding
+    j = np.where((1 << j) > ln[idx], j - 1, j)
+    for lev in np.unique(j):
+        sel = idx[j == lev]
+        t = table[lev]
+        out[sel] = np.maximum(t[lo[sel]], t[hi[sel] - (1 << lev)])
+    return out
+
+
 def chunk_flags(y_edge: np.ndarray, q_edge: np.ndarray, *, out_begin: int, first_start: int,
                 n_frames: int, n_fft: int, hop: int, norm: str,
                 chunk_lo: Sequence[int], chunk_hi: Sequence[int],
@@ -102,24 +128,23 @@ def chunk_flags(y_edge: np.ndarray, q_edge: np.ndarray, *, out_begin: int, first
     if len(gq):
         lo_i = np.searchsorted(gq, q_edge - n_fft, "left")
         hi_i = np.searchsorted(gq, q_edge + n_fft, "right")
-        # running max via a sparse table would be faster; edges are <= 4*n_fft long
-        for t in range(len(q_edge)):
-            if hi_i[t] > lo_i[t]:
-                A[t] = gy[lo_i[t]:hi_i[t]].max()
+        A = _range_max(gy, lo_i, hi_i)
     D = 2.0 * (KAPPA_INT * A + KAPPA_EDGE * A * s1 / _den(s2, norm))
     out = []
     nc = len(peaks)
+    # q_edge is sorted: chunk c's edge samples are one slice of it
+    ia = np.searchsorted(q_edge, np.asarray(chunk_lo, np.int64), "left")
+    ib = np.searchsorted(q_edge, np.asarray(chunk_hi, np.int64), "left")
     for c in range(nc):
         P = float(peaks[c])
-        a, b = int(chunk_lo[c]), int(chunk_hi[c])
-        m = (q_edge >= a) & (q_edge < b)
+        m = slice(int(ia[c]), int(max(ia[c], ib[c])))
         # interior samples: full window sums (S1/S2 <= 1.5 for the overlaps used)
         amp_int = max(float(peaks[max(c - 1, 0)]), P, float(peaks[min(c + 1, nc - 1)]))
         d_int = 2.0 * (KAPPA_INT + 1.5 * KAPPA_EDGE) * amp_int
         hi = P + d_int
         lo = P - d_int
         edge_peak = 0.0
-        if m.any():
+        if m.stop > m.start:
             ye, de = y_edge[m], D[m]
             edge_peak = float(ye.max())
             hi = max(hi, float((ye + de).max()))

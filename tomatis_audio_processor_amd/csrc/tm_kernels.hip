@@ -253,12 +253,18 @@ __global__ __launch_bounds__(256) void k_levels_any(const float* __restrict__ x,
 // Streaming levels (hop % 128 == 0): numpy's pairwise mean over a power-of-two
 // frame is a perfect binary tree over 128-sample leaves aligned to the frame
 // start, so every 128-sample block (aligned to first_start) has ONE leaf sum
-// shared by all frames covering it.  k_leaves: lane = (block b, accumulator
-// chain c) over 8 blocks per wave; chain c sums m^2 of samples c, c+8, ..c+120
-// in order (numpy's 8 accumulators); the 8 chains combine as
+// shared by all frames covering it.  k_leaves: one wave per group of 8 blocks
+// (1024 samples) of one stream (blockIdx.y); the group is read with 16-byte
+// lane-contiguous loads (1 KB per load instruction), every sample's m^2 goes
+// to LDS in chain order, then lane (block b, chain c) sums m^2 of samples c,
+// c+8, .., c+120 in order (numpy's 8 accumulators) and the 8 chains combine as
 // ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) via xor-shuffles (IEEE add commutes).
+// (The first form, each lane loading its own chain's 8-byte samples, ran at
+// 3.0 TB/s on C5x: 0.61 ms for 1.84 GB.)
 // k_frame_r: per frame, perfect-tree sum of n_fft/128 leaves, mean, sqrt.
 // ---------------------------------------------------------------------------
+constexpr int kLfC = 24;          // LDS stride of a chain (16 values + pad: conflict-free writes)
+constexpr int kLfB = 8 * kLfC + 4;  // LDS stride of a block
 template <typename T, int CH>
 __global__ __launch_bounds__(256) void k_leaves(const float* __restrict__ x,
                                                 const TomatisStream* __restrict__ st,
@@ -266,51 +272,60 @@ __global__ __launch_bounds__(256) void k_leaves(const float* __restrict__ x,
                                                 const int64_t* __restrict__ grp_base,
                                                 const int64_t* __restrict__ leaf_base,
                                                 int64_t n_groups, T* __restrict__ leaves) {
+  __shared__ T sm[4][8 * kLfB];
   const int lane = threadIdx.x & 63;
-  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // 8-block group
-  if (g >= n_groups) return;
-  int lo = 0, hi = n_streams - 1;  // stream of this group (wave-uniform)
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (grp_base[mid] <= g) lo = mid;
-    else hi = mid - 1;
-  }
+  T* const w = sm[threadIdx.x >> 6];
+  const int lo = blockIdx.y;  // stream
+  const int64_t gl = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // 8-block group of the stream
+  if (lo >= n_streams || gl >= grp_base[lo + 1] - grp_base[lo]) return;
+  (void)n_groups;
   const TomatisStream S = st[lo];
-  const int64_t gl = g - grp_base[lo];
-  const int b = lane >> 3, c = lane & 7;
-  const int64_t blk = gl * 8 + b;
   const int64_t nblk = leaf_base[lo + 1] - leaf_base[lo];
   const int64_t p0 = S.first_start + gl * 1024;  // first sample of the group
   const T scale = (T)S.in_scale;
   const float* xs = x + S.in_off;
-  T acc = (T)0;
-  if (p0 >= 0 && p0 + 1024 <= S.n) {
-    T m2[16];
+  // sample i of the group -> block i >> 7, chain i & 7, position (i >> 3) & 15
+  auto slot = [&](int i) -> T& { return w[(i >> 7) * kLfB + (i & 7) * kLfC + ((i >> 3) & 15)]; };
+  const bool full = p0 >= 0 && p0 + 1024 <= S.n && ((uintptr_t)(xs + p0 * CH) & 15) == 0;
+  if (full) {
+    const float4* x4 = reinterpret_cast<const float4*>(xs + p0 * CH);
+    constexpr int NL = 1024 * CH / 4 / 64;  // float4 per lane: 8 (stereo) / 4 (mono)
+    float4 t[NL];
 #pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const int64_t p = p0 + 128 * b + c + 8 * t;
+    for (int u = 0; u < NL; ++u) t[u] = x4[u * 64 + lane];  // all loads in flight
+#pragma unroll
+    for (int u = 0; u < NL; ++u) {
+      const int f = u * 64 + lane;  // float4 index within the group
       if constexpr (CH == 2) {
-        const float2 u = reinterpret_cast<const float2*>(xs)[p];
-        const float v[2] = {u.x, u.y};
-        m2[t] = msq_of<T>(v, 2, scale);
+        const float a0[2] = {t[u].x, t[u].y}, a1[2] = {t[u].z, t[u].w};
+        slot(2 * f) = msq_of<T>(a0, 2, scale);
+        slot(2 * f + 1) = msq_of<T>(a1, 2, scale);
       } else {
-        m2[t] = msq_of<T>(xs + p, 1, scale);
+        const float a[4] = {t[u].x, t[u].y, t[u].z, t[u].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) slot(4 * f + e) = msq_of<T>(a + e, 1, scale);
       }
     }
-    acc = m2[0];
-#pragma unroll
-    for (int t = 1; t < 16; ++t) acc = acc + m2[t];
-  } else {
-    for (int t = 0; t < 16; ++t) {
-      const int64_t p = p0 + 128 * b + c + 8 * t;
-      const T m = (p >= 0 && p < S.n) ? msq_of<T>(xs + p * CH, CH, scale) : (T)0;
-      acc = (t == 0) ? m : acc + m;
+  } else {  // a stream edge (zeros outside the stream) or an unaligned stream: per sample
+#pragma unroll 4
+    for (int i = lane; i < 1024; i += 64) {
+      const int64_t p = p0 + i;
+      slot(i) = (p >= 0 && p < S.n) ? msq_of<T>(xs + p * CH, CH, scale) : (T)0;
     }
   }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int b = lane >> 3, c = lane & 7;
+  const T* ch = w + b * kLfB + c * kLfC;
+  T acc = ch[0];
+#pragma unroll
+  for (int q = 1; q < 16; ++q) acc = acc + ch[q];
   // pairwise tree over the 8 chains of a block
   acc = acc + __shfl_xor(acc, 1, 64);
   acc = acc + __shfl_xor(acc, 2, 64);
   acc = acc + __shfl_xor(acc, 4, 64);
+  const int64_t blk = gl * 8 + b;
   if (c == 0 && blk < nblk) leaves[leaf_base[lo] + blk] = acc;
 }
 
@@ -1713,6 +1728,7 @@ struct tomatis_plan_s {
   // streaming levels (hop % 128 == 0): per-stream 8-block groups and leaves
   bool leaf_path = false;
   int64_t n_groups = 0;
+  int64_t max_groups = 0;          // most groups of one stream (k_leaves grid x)
   int64_t* grp_base = nullptr;
   int64_t* leaf_base = nullptr;
   void* leaves = nullptr;
@@ -2059,6 +2075,7 @@ static int plan_build(tomatis_plan_s* p, const float* window) {
       const int64_t nblk = F > 0 ? ((F - 1) * hop + N) / 128 : 0;
       lbase[s + 1] = lbase[s] + nblk;
       gb[s + 1] = gb[s] + (nblk + 7) / 8;
+      p->max_groups = std::max<int64_t>(p->max_groups, (nblk + 7) / 8);
     }
     p->n_groups = gb[ns];
     if ((rc = dalloc_copy(&p->grp_base, gb))) return rc;
@@ -2404,7 +2421,7 @@ int tomatis_levels(tomatis_plan_t p, const float* x, void* r_out, int32_t prec, 
     return launch_check();
   }
   if (p->leaf_path && (prec == TOMATIS_F32 || prec == TOMATIS_F64)) {
-    const unsigned gblk = (unsigned)((p->n_groups + 3) / 4);
+    const dim3 gblk((unsigned)((p->max_groups + 3) / 4), (unsigned)p->n_streams);
     const unsigned fblk = (unsigned)((p->total_frames + 255) / 256);
     const int ch = p->d.ch, N = p->d.n_fft, hop = p->d.hop, ns = p->n_streams;
     if (prec == TOMATIS_F32) {
