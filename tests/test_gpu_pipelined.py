@@ -216,8 +216,8 @@ def test_pipelined_two_pass(case):
     _check(torch, F, (res.y, res.chunk_peaks, held[2], held[3]), refs[-1][:4], len(xs) - 1)
 
 
-@pytest.mark.parametrize("groups", [1, 2])
-def test_pipelined_adaptive(groups):
+@pytest.mark.parametrize("groups,second", [(1, True), (2, True), (2, False)])
+def test_pipelined_adaptive(groups, second):
     """Adaptive batches (AdaptiveGroups, src/process_tomatis_adaptive.py): the
     global limiter of pass k applied inside pass k+1's transforms
     (tomatis_stft_ola_pipelined), a different input per pass (attenuation and
@@ -235,7 +235,7 @@ def test_pipelined_adaptive(groups):
         res = ref.run()
         refs.append((res.y.clone(), res.chunk_peaks.clone(), res.states.clone(), res.alpha.clone()))
     del ref
-    pipe = E.AdaptiveGroups(ss, groups=groups, pipelined=True, **kw)
+    pipe = E.AdaptiveGroups(ss, groups=groups, pipelined=True, second_buffer=second, **kw)
     held = None
     for k, x in enumerate(xs):
         ss.x.copy_(x)

@@ -81,8 +81,9 @@ def _make_pipe(engine, args, ss, n_files, pipelined):
     params = dict(n_fft=args.n_fft, hop=args.hop)
     if args.mode == "adaptive":   # >= 4 files: two interleaved stream groups
         if n_files >= 4:
-            return engine.AdaptiveGroups(ss, groups=2, pipelined=pipelined, **params)
-        return engine.AdaptivePipeline(ss, pipelined=pipelined, **params)
+            return engine.AdaptiveGroups(ss, groups=2, pipelined=pipelined, second_buffer=False,
+                                         **params)
+        return engine.AdaptivePipeline(ss, pipelined=pipelined, second_buffer=False, **params)
     if args.mode == "xfade":
         return engine.GatePipeline(ss, gate_ui=args.gate_ui, gate_offset=args.gate_offset,
                                    xfade_ms=args.xfade_ms, pipelined=pipelined,

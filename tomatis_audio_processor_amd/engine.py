@@ -725,12 +725,13 @@ class AdaptivePipeline:
     def __init__(self, ss: StreamSet, *, fc=1000.0, slope=12.0, c1_low=15.0, c1_high=-15.0,
                  c2_low=-15.0, c2_high=15.0, target_c2=0.5, hyst_db=3.0, min_hold_ms=250.0,
                  xfade_ms=500.0, headroom_margin=2.0, n_fft=4096, hop=2048, out=None,
-                 pipelined=False, out2=None):
+                 pipelined=False, out2=None, second_buffer=True):
         """``out``: optional (y, offsets) output buffer shared with other
         pipelines (AdaptiveGroups).  ``pipelined``: a batch pipeline as
         GatePipeline's (tomatis_stft_ola_pipelined: each pass's transform
         applies the previous pass's global limiter; ``out2`` the second output
-        buffer, same offsets, when ``out`` is shared)."""
+        buffer, same offsets, when ``out`` is shared; ``second_buffer=False``:
+        none until a second pass of this pipeline needs it)."""
         torch = _torch()
         _check_fft(n_fft, hop, ss.ch)
         self.ss, self.n_fft, self.hop = ss, n_fft, hop
@@ -792,7 +793,8 @@ class AdaptivePipeline:
         self.pending = False      # pipelined: self.y awaits its limiter
         self._after = None        # run(prev_pipe=...): another pipeline's pending pass
         if self.pipelined:
-            self._ys = [self.y, out2 if out2 is not None else torch.empty_like(self.y)]
+            self._ys = [self.y, out2 if out2 is not None else
+                        (torch.empty_like(self.y) if second_buffer else None)]
             self._pks = [self.peaks, torch.zeros_like(self.peaks)]
             self._cur = 0
 
@@ -831,7 +833,11 @@ class AdaptivePipeline:
 
     def _pipelined_pass(self) -> bool:
         a = self._after
-        nxt = 1 - self._cur   # (AdaptiveGroups: every group alternates in step)
+        # the other buffer while this pipeline's own previous pass is pending,
+        # else the current one (AdaptiveGroups: every group alternates in step)
+        nxt = (1 - self._cur) if self.pending else self._cur
+        if self._ys[nxt] is None:  # second_buffer=False, standalone: allocated on first need
+            self._ys[nxt] = _torch().empty_like(self._ys[self._cur])
         if a is not None and a.pending:
             pplan, prev_y, prev_pk = a.plan, a.y, a.peaks
         elif self.pending:
@@ -1076,15 +1082,18 @@ class AdaptiveGroups:
     one: a fused-limiter launch never shares the dispatcher with another).
     Output in one buffer; ``result()`` merges the groups."""
 
-    def __init__(self, ss: StreamSet, groups: int = 2, pipelined=False, **params):
+    def __init__(self, ss: StreamSet, groups: int = 2, pipelined=False, second_buffer=True,
+                 **params):
         """``pipelined``: every group pipelines its passes (AdaptivePipeline);
-        the groups alternate between two shared output buffers in step."""
+        the groups alternate between two shared output buffers in step
+        (``second_buffer=False``: the second one allocated when a second pass
+        needs it -- batch.py's single-pass batches never do)."""
         torch = _torch()
         n_fft, hop = params.get("n_fft", 4096), params.get("hop", 2048)
         G = max(1, min(int(groups), ss.n_streams))
         out_lens = [N if dsp.adaptive_frames(N, n_fft, hop)[1] else 0 for N in ss.lens]
         self.y, offs = _alloc_out(torch, out_lens, ss.ch, ss.x.device)
-        y2 = torch.empty_like(self.y) if pipelined else None
+        y2 = torch.empty_like(self.y) if (pipelined and second_buffer) else None
         # contiguous groups balanced by samples
         tot, acc, cuts = float(sum(ss.lens)) or 1.0, 0, [0]
         for i, N in enumerate(ss.lens):
@@ -1101,7 +1110,7 @@ class AdaptiveGroups:
         for g, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
             sub = StreamSet(x=ss.x, offs=ss.offs[a:b], lens=ss.lens[a:b], ch=ss.ch, sr=ss.sr)
             p = AdaptivePipeline(sub, out=(self.y, offs[a:b]), pipelined=pipelined, out2=y2,
-                                 **params)
+                                 second_buffer=False, **params)
             p.stream = torch.cuda.Stream()
             serial = mh_mode == "serial" or (mh_mode == "auto" and chain and g > 0)
             p.plan.set_option(OPT_MINHOLD_SERIAL, int(serial))
@@ -1123,6 +1132,11 @@ class AdaptiveGroups:
                 cur.wait_stream(q.stream or cur)
         for p in self.pipes:
             p.stream.wait_stream(cur)
+            if p.pipelined and p.pending and p._ys[1 - p._cur] is None:
+                # the groups' shared second buffer, on the first pass that needs it
+                y2 = torch.empty_like(self.pipes[0]._ys[0])
+                for q in self.pipes:
+                    q._ys[1] = y2
         G = len(self.pipes)
         gens = []
         # transforms in group order; the first also waits for every group's
