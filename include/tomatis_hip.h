@@ -62,7 +62,7 @@
 extern "C" {
 #endif
 
-#define TOMATIS_ABI_VERSION 10
+#define TOMATIS_ABI_VERSION 11
 
 #define TOMATIS_OK 0
 #define TOMATIS_E_ARG (-1)        /* bad argument */
@@ -250,15 +250,23 @@ int tomatis_stft_ola_limited_edges(tomatis_plan_t plan, const float* x, const fl
  * state from the samples it loads for the FFT and picks the gain row from it.
  * r_out (f32) and states_out (1 = C1, 2 = C2) per frame as tomatis_levels /
  * tomatis_gate_std write them; n_rows must be 2 (rows C1, C2); limit 0 = no
- * limiter.  TOMATIS_E_UNSUPPORTED unless n_fft 2048, hop 256 or 512, <= 2
- * channels, alpha_mode 0, in_scale 1 and every stream below 2^31 bytes (the
- * caller runs the two-pass chain).  When a run's look-back does not resolve
+ * limiter.  TOMATIS_E_UNSUPPORTED unless n_fft 2048 with hop 256 or 512 and
+ * alpha_mode 0, or (dev option TOMATIS_DEV_FUSED_4096 set: measured slower than
+ * the two-pass chain) n_fft 4096 with hop 1024 and alpha_mode 0 or 1, <= 2
+ * channels, in_scale 1 and every stream below 2^31 bytes (the caller runs the
+ * two-pass chain).  alpha_mode 1 (cross-fade, src/process_tomatis_xfade.py:
+ * 237-278): the rows are tomatis_gate_std's (0 = g1, 1 = g2, 2 + m = alpha
+ * m / xfade_frames) and every frame's alpha goes to the array set by
+ * tomatis_plan_set_gate_alpha (as tomatis_gate_std's alpha_out).  When a run's look-back does not resolve
  * within 512 frames the launch sets TOMATIS_ERR_GATE_CARRY and its outputs are
  * invalid: the caller re-runs the two-pass chain.  Replaces
  * src/process_tomatis.py:373-385 (levels + gate loop) feeding :391-400. */
 int tomatis_stft_ola_gated(tomatis_plan_t plan, const float* x, const float* gain_rows,
                            int32_t n_rows, float* y, uint32_t* chunk_peak_bits, float limit,
                            float* r_out, uint8_t* states_out, void* hip_stream);
+/* Cross-fade plans (alpha_mode 1): the float64 per-frame alpha output of the
+ * gated calls (required before one; frame-major as tomatis_gate_std's).  ABI 11. */
+int tomatis_plan_set_gate_alpha(tomatis_plan_t plan, double* alpha_out);
 /* The two launches of tomatis_stft_ola_gated separately (the caller times the
  * transform alone): tomatis_gate_lookback runs the look-back pre-kernel on x;
  * tomatis_stft_ola_gated_after_lookback then runs the transform on the same x,
@@ -392,6 +400,7 @@ int tomatis_plan_set_option(tomatis_plan_t plan, int32_t option, int64_t value);
 #define TOMATIS_DEV_WG 12
 #define TOMATIS_DEV_SLOTS 13           /* resident run slots assumed by the plan (0: the device's) */
 #define TOMATIS_DEV_FUSED_LEVELS 14    /* 0: tomatis_stft_ola_gated declines (host two-pass) */
+#define TOMATIS_DEV_FUSED_4096 15      /* 1: the gated calls take n_fft 4096 / hop 1024 (slower) */
 int tomatis_set_dev_option(int32_t key, int32_t value);
 /* The current override of key (-1: default, or an unknown key). */
 int32_t tomatis_get_dev_option(int32_t key);

@@ -77,8 +77,11 @@ def _result_of(E, pipe, y, peaks, r, states, alpha):
 
 
 def _gate_passes(torch, E, ss, xs, kw, check_mid):
-    """unpipelined references, then the pipelined passes compared as each
-    becomes final; check_mid(res) on the middle pass's Result"""
+    """unpipelined references, then the pipelined passes as bench.py's timed
+    loop runs them: back to back with no host synchronisation.  Each pass's
+    arrays are copied on the stream once final (its output after the next
+    pass, its r / states after its own) and compared at the end;
+    check_mid(res) on the middle pass."""
     ref = E.GatePipeline(ss, **kw)
     refs = []
     for x in xs:
@@ -89,9 +92,19 @@ def _gate_passes(torch, E, ss, xs, kw, check_mid):
     del ref
     pipe = E.GatePipeline(ss, pipelined=True, **kw)
     F = pipe.plan.total_frames
-    held = None
-
-    def same(k, y, pk, r, st, al):
+    got, cur = [], None
+    for k, x in enumerate(xs):
+        _set(pipe, x)
+        assert pipe.run(check_device=False) is None and pipe.pending and pipe.pipelined
+        if cur is not None:    # pass k-1 was limited inside pass k's transform
+            got.append((cur[0].clone(), cur[1].clone()) + cur[2:])
+        cur = (pipe.y, pipe.peaks, pipe.r.clone(), pipe.states.clone(),
+               pipe.alpha.clone() if pipe.alpha is not None else None)
+    res = pipe.result()
+    got.append((res.y, res.chunk_peaks) + cur[2:])
+    assert pipe.finish() == 0 and not pipe.pending
+    assert pipe.gate_fallbacks == 0
+    for k, (y, pk, r, st, al) in enumerate(got):
         ry, rpk, rr, rst, ral = refs[k]
         assert torch.equal(st[:F], rst[:F]), f"pass {k}: states differ"
         assert torch.equal(r[:F].view(torch.int32), rr[:F].view(torch.int32)), f"pass {k}: r differs"
@@ -99,21 +112,7 @@ def _gate_passes(torch, E, ss, xs, kw, check_mid):
             assert torch.equal(al[:F], ral[:F]), f"pass {k}: alpha differs"
         assert torch.equal(pk, rpk), f"pass {k}: chunk peaks differ"
         assert torch.equal(y, ry), f"pass {k}: output differs"
-
-    for k, x in enumerate(xs):
-        _set(pipe, x)
-        assert pipe.run() is None and pipe.pending and pipe.pipelined
-        if held is not None:
-            same(k - 1, *held)
-            if k - 1 == 1:
-                y, pk, r, st, al = held
-                check_mid(_result_of(E, pipe, y, pk, r, st, al))
-        held = (pipe.y, pipe.peaks, pipe.r.clone(), pipe.states.clone(),
-                pipe.alpha.clone() if pipe.alpha is not None else None)
-    assert pipe.gate_fallbacks == 0
-    res = pipe.result()
-    assert not pipe.pending
-    same(len(xs) - 1, res.y, res.chunk_peaks, held[2], held[3], held[4])
+    check_mid(_result_of(E, pipe, *got[1]))
     return pipe
 
 

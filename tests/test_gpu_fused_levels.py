@@ -220,11 +220,13 @@ def test_gated_hovering_stream_in_c4_batch():
 
 
 def test_gated_declines_other_shapes():
-    """Shapes outside the fused gate (n_fft 4096, hop 1024, xfade) run two passes."""
+    """Shapes outside the fused gate (n_fft 4096 unless TOMATIS_DEV_FUSED_4096,
+    n_fft 2048 with hop 1024, cross-fade at 2048) run two passes."""
     torch, E = _engine()
     sr, n = 44100, 44100 * 20
     ss = E.StreamSet.synthetic(1, n, 2, sr, seed0=5)
-    for kw in (dict(n_fft=4096, hop=1024), dict(n_fft=2048, hop=1024),
+    for kw in (dict(n_fft=4096, hop=1024), dict(n_fft=4096, hop=1024, xfade_ms=500.0),
+               dict(n_fft=4096, hop=2048), dict(n_fft=2048, hop=1024),
                dict(n_fft=2048, hop=512, xfade_ms=500.0)):
         pipe = E.GatePipeline(ss, gate_ui=50, **kw)
         pipe.run()

@@ -31,7 +31,7 @@ def test_library_exports_all_symbols():
     missing = [n for n in declared() if not hasattr(h, n)]
     assert not missing, missing
     assert set(_lib.EXPORTS) == set(declared())
-    assert h.tomatis_abi_version() == _lib.ABI_VERSION == 10
+    assert h.tomatis_abi_version() == _lib.ABI_VERSION == 11
     h.tomatis_status_string.restype = ctypes.c_char_p
     assert h.tomatis_status_string(-2).decode().startswith("configuration")
 

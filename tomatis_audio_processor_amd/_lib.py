@@ -14,7 +14,7 @@ import ctypes as C
 import os
 
 LIB_NAME = "libtomatis_hip.so"
-ABI_VERSION = 10  # include/tomatis_hip.h TOMATIS_ABI_VERSION
+ABI_VERSION = 11  # include/tomatis_hip.h TOMATIS_ABI_VERSION
 GATE_SEGMENT = 1024      # TOMATIS_GATE_SEGMENT
 GATE_NONE = -536870912   # TOMATIS_GATE_NONE
 ERR_LIMITER_WAIT = 1     # TOMATIS_ERR_LIMITER_WAIT
@@ -27,7 +27,7 @@ OPT_MINHOLD_SERIAL = 3   # TOMATIS_OPT_MINHOLD_SERIAL
 # development overrides (TOMATIS_DEV_*: tests and A/B experiments only)
 DEV_KEYS = dict(FAST_LOOP=1, RUN_ROUNDS=2, RUN_FRAMES=3, LEVELS_LEGACY=4, GATE_TF=5, MH_PARTS=6,
                 FORCE_LDS=7, P64=8, ALPHA_SEQ=9, GAIN_LDS=10, FUSE_LIMITER=11, WG=12,
-                SLOTS=13, FUSED_LEVELS=14)
+                SLOTS=13, FUSED_LEVELS=14, FUSED_4096=15)
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 F32, F64 = 0, 1
@@ -100,6 +100,7 @@ _SIGS = {
     "tomatis_apply_limiter_edges": (C.c_int, [_P, _P, _P, C.c_float, C.c_int32, _P]),
     "tomatis_stft_ola_gated": (C.c_int, [_P, _P, _P, C.c_int32, _P, _P, C.c_float, _P, _P, _P]),
     "tomatis_gate_lookback": (C.c_int, [_P, _P, _P]),
+    "tomatis_plan_set_gate_alpha": (C.c_int, [_P, _P]),
     "tomatis_flacd_workspace_bytes": (C.c_int64, [C.c_int64, C.c_int32]),
     "tomatis_flacd_plan": (C.c_int, [_P, C.c_int64, C.c_int32, C.c_int32, _P, _P, _P]),
     "tomatis_flacd_write": (C.c_int, [_P, C.c_int64, C.c_int32, C.c_int32, _P, _P, _P, _P]),

@@ -37,4 +37,18 @@ __device__ __forceinline__ int gate_step(int id, uint8_t pr, int D) {
   return 0;
 }
 
+// cross-fade alpha (process_tomatis_xfade.py:251-274), float64 exactly as the
+// reference: +-step toward the target (0 in C1, 1 in C2), snapped once within
+// a step (callers: a = xf > 0 ? alpha_step(a, tgt, 1.0 / xf) : tgt)
+__device__ __forceinline__ double alpha_step(double a, double tgt, double step) {
+  const double d = tgt - a;
+  if (fabs(d) <= step) return tgt;
+  return a + step * (d > 0 ? 1.0 : (d < 0 ? -1.0 : 0.0));
+}
+// gain row of an alpha: the pure rows 0 (C1) / 1 (C2), else lattice row 2 + m
+__device__ __forceinline__ uint16_t xfade_row(double a, int xf) {
+  if (xf > 0 && a > 0.0 && a < 1.0) return (uint16_t)(2 + (int)rint(a * xf));
+  return (a < 0.5) ? 0 : 1;
+}
+
 }  // namespace tgate

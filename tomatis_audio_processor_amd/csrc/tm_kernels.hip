@@ -609,11 +609,7 @@ __global__ void k_ts_carry(const int32_t* __restrict__ all, int rank, int D, int
 // ===========================================================================
 // alpha scans (sequential per stream; f64 exactly as the reference)
 // ===========================================================================
-__device__ __forceinline__ double alpha_step(double a, double tgt, double step) {
-  const double d = tgt - a;
-  if (fabs(d) <= step) return tgt;
-  return a + step * (d > 0 ? 1.0 : (d < 0 ? -1.0 : 0.0));
-}
+// alpha_step, xfade_row: tm_gate.h
 
 // xfade (process_tomatis_xfade.py:251-274): alpha starts at 0.0.
 // xfade alpha (process_tomatis_xfade.py:251-274) in three passes over the gate
@@ -624,10 +620,6 @@ __device__ __forceinline__ double alpha_step(double a, double tgt, double step) 
 // "sync" frame on, alpha depends only on the states; only the prefix before it
 // needs the previous segment's final alpha.  Every value is produced by the
 // same float64 operations in the same order as the sequential reference loop.
-__device__ __forceinline__ uint16_t xfade_row(double a, int xf) {
-  if (xf > 0 && a > 0.0 && a < 1.0) return (uint16_t)(2 + (int)rint(a * xf));
-  return (a < 0.5) ? 0 : 1;
-}
 
 // pass 1: one wave per segment: sync frame, alpha from it to the segment end.
 // The segment's states are staged in LDS by all lanes; the recurrence runs in
@@ -1713,6 +1705,8 @@ struct tomatis_plan_s {
   int32_t* gate_carry = nullptr;
   int gate_cap = 0;
   uint16_t* gate_tf = nullptr;     // chained runs' transfer tables [gate_cap][D + 2]
+  double* gate_acarry = nullptr;   // cross-fade: alpha before each run's first frame
+  double* gate_aout = nullptr;     // cross-fade: the caller's per-frame alpha (set_gate_alpha)
   // the look-back the carries in gate_carry belong to (input, run layout)
   const float* gl_x = nullptr;
   int gl_gen = -1;
@@ -1773,8 +1767,8 @@ int launch_check() { return hipfail(hipGetLastError()); }
 
 namespace tshared {
 // development overrides (tomatis_set_dev_option); -1 = the default
-constexpr int kDevKeys = 15;
-static int g_dev[kDevKeys] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+constexpr int kDevKeys = 16;
+static int g_dev[kDevKeys] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 int dev_opt(int key, int dflt) {
   const int v = (key > 0 && key < kDevKeys) ? g_dev[key] : -1;
   return v < 0 ? dflt : v;
@@ -1806,7 +1800,7 @@ int tomatis_plan_destroy(tomatis_plan_t p) {
                   p->aq, p->afin, p->acin,
                   p->chunk_need, p->chunk_done, p->chunk_rng, p->err, p->twL,
                   p->xs_pieces, p->gate_carry,
-                  p->gate_tf,
+                  p->gate_tf, p->gate_acarry,
                   p->pw_leaf, p->pw_prog, p->blue_b, p->blue_h, p->glb_work};
   for (void* q : ptrs) dfree(q);
   delete p;
@@ -2659,16 +2653,21 @@ struct GateOut {
 static int gate_lookback(tomatis_plan_s* p, const float* x, hipStream_t s) {
   const int nst = p->d.up_delay_frames + 2;
   const bool chain = nst <= kGateChainStates;
+  const bool xa = p->d.alpha_mode == 1;
   if (p->n_runs > p->gate_cap) {
     dfree(p->gate_carry);
     dfree(p->gate_tf);
+    dfree(p->gate_acarry);
     p->gate_carry = nullptr;
     p->gate_tf = nullptr;
+    p->gate_acarry = nullptr;
     p->gate_cap = 0;
     if (hipMalloc(reinterpret_cast<void**>(&p->gate_carry), (size_t)p->n_runs * sizeof(int32_t)))
       return TOMATIS_E_NOMEM;
     if (chain && hipMalloc(reinterpret_cast<void**>(&p->gate_tf),
                            (size_t)p->n_runs * nst * sizeof(uint16_t)))
+      return TOMATIS_E_NOMEM;
+    if (xa && hipMalloc(reinterpret_cast<void**>(&p->gate_acarry), (size_t)p->n_runs * sizeof(double)))
       return TOMATIS_E_NOMEM;
     p->gate_cap = p->n_runs;
   }
@@ -2684,7 +2683,10 @@ static int gate_lookback(tomatis_plan_s* p, const float* x, hipStream_t s) {
   A.hop = p->d.hop;
   A.ch = p->d.ch;
   A.gate_D = p->d.up_delay_frames;
-  launch_gate_carry(A, p->P, p->SH, p->d.ch, p->gate_carry, chain ? p->gate_tf : nullptr, s);
+  A.gate_xf = xa ? p->d.xfade_frames : -1;
+  A.gate_astep = (xa && p->d.xfade_frames > 0) ? 1.0 / p->d.xfade_frames : 1.0;
+  launch_gate_carry(A, p->P, p->SH, p->d.ch, p->gate_carry, (chain && !xa) ? p->gate_tf : nullptr,
+                    p->gate_acarry, s);
   return launch_check();
 }
 
@@ -2820,6 +2822,9 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
   A.st_out = nullptr;
   A.gcarry = nullptr;
   A.gtf = nullptr;
+  A.gate_xf = -1;
+  A.a_out = nullptr;
+  A.gacarry = nullptr;
   A.yprev = nullptr;
   A.peaks_prev = nullptr;
   A.runs_prev = p->runs;
@@ -2840,6 +2845,13 @@ static int stft_ola_impl(tomatis_plan_t p, const float* x, const float* gains, i
     A.st_out = gate->states;
     A.gcarry = p->gate_carry;
     A.gtf = (p->d.up_delay_frames + 2 <= kGateChainStates) ? p->gate_tf : nullptr;
+    if (p->d.alpha_mode == 1) {  // cross-fade (n_fft 4096): alpha in-kernel
+      A.gate_xf = p->d.xfade_frames;
+      A.gate_astep = p->d.xfade_frames > 0 ? 1.0 / p->d.xfade_frames : 1.0;
+      A.a_out = p->gate_aout;
+      A.gacarry = p->gate_acarry;
+      A.gtf = nullptr;
+    }
   }
   if (limit > 0.f) {
     if (!p->chunk_done) return TOMATIS_E_UNSUPPORTED;
@@ -2956,19 +2968,35 @@ int tomatis_stft_ola_limited_edges(tomatis_plan_t p, const float* x, const float
 }
 
 // tomatis_stft_ola_gated eligibility: the fused kernel's interior loop at
-// n_fft 2048 with hop 256 / 512 (the 16-leaf window spans whole hop blocks),
-// the standard gate (two rows), float input used as is, and every stream
-// addressable by the 31-bit buffer offsets of k_gate_carry's loads
+// n_fft 2048 with hop 256 / 512 (the 16-leaf window spans whole hop blocks)
+// and the standard gate (two rows), or its two-wave frames at n_fft 4096 with
+// hop 1024 and the standard gate or the cross-fade (alpha in-kernel); float
+// input used as is, and every stream addressable by the 31-bit buffer offsets
+// of k_gate_carry's loads
 static bool gated_eligible(const tomatis_plan_s* p) {
   const TomatisPlanDesc& d = p->d;
   if (dev_opt(TOMATIS_DEV_FUSED_LEVELS, 1) == 0) return false;
-  if (p->generic || p->lds || p->P != 64 || p->NR != 32 || d.n_fft != 2048) return false;
-  if (!(p->SH == 4 || p->SH == 8) || d.ch < 1 || d.ch > 2 || d.alpha_mode != 0) return false;
+  if (p->generic || p->lds || p->NR != 32 || d.ch < 1 || d.ch > 2) return false;
+  const bool f2048 = p->P == 64 && d.n_fft == 2048 && (p->SH == 4 || p->SH == 8) && d.alpha_mode == 0;
+  // (n_fft 4096: measured slower than the two-pass chain -- the level pass's
+  // HBM read costs less than the level arithmetic inside the two-wave frame
+  // loop, DESIGN.md §6 "Fused levels at 4096" -- so opt-in)
+  const bool f4096 = dev_opt(TOMATIS_DEV_FUSED_4096, 0) != 0 &&
+                     p->P == 128 && d.n_fft == 4096 && p->SH == 8 && kFftX &&
+                     (d.alpha_mode == 0 || d.alpha_mode == 1) &&
+                     transform_wg(p->P, p->NR) == 512;
+  if (!(f2048 || f4096)) return false;
   for (int s = 0; s < p->n_streams; ++s) {
     const TomatisStream& S = p->hs[s];
     if (S.in_scale != 1.f || S.n * d.ch * 4 > 0x7fffffffll) return false;
   }
   return true;
+}
+
+int tomatis_plan_set_gate_alpha(tomatis_plan_t p, double* alpha_out) {
+  if (!p) return TOMATIS_E_ARG;
+  p->gate_aout = alpha_out;
+  return TOMATIS_OK;
 }
 
 int tomatis_gate_lookback(tomatis_plan_t p, const float* x, void* hs) {
@@ -2977,12 +3005,20 @@ int tomatis_gate_lookback(tomatis_plan_t p, const float* x, void* hs) {
   return gate_lookback(p, x, (hipStream_t)hs);
 }
 
+// gain rows of a gated call: g1, g2 (standard); cross-fade: g1, g2 and the
+// alpha lattice 0, 1/xf, ..., 1 (rows 2 + m), with the caller's alpha output set
+static bool gated_rows_ok(const tomatis_plan_s* p, int32_t n_rows) {
+  if (p->d.alpha_mode != 1) return n_rows == 2;
+  return p->gate_aout && n_rows >= 2 + std::max(2, p->d.xfade_frames + 1);
+}
+
 static int stft_ola_gated(tomatis_plan_t p, const float* x, const float* gains, int32_t n_rows,
                           float* y, uint32_t* peaks, float limit, float* r_out,
                           uint8_t* states_out, bool lookback_done, void* hs) {
-  if (!p || !x || !gains || !y || !peaks || !r_out || !states_out || n_rows != 2 || limit < 0.f)
+  if (!p || !x || !gains || !y || !peaks || !r_out || !states_out || limit < 0.f)
     return TOMATIS_E_ARG;
   if (!gated_eligible(p)) return TOMATIS_E_UNSUPPORTED;
+  if (!gated_rows_ok(p, n_rows)) return TOMATIS_E_ARG;
   const GateOut g{r_out, states_out, lookback_done};
   if (!(limit > 0.f)) return stft_ola_impl(p, x, gains, n_rows, nullptr, y, peaks, 0.f, hs, &g);
   const bool fuse = p->chunk_done && p->fuse_span > 0 && p->fuse_enabled &&
@@ -3019,13 +3055,15 @@ int tomatis_stft_ola_gated_pipelined_after(tomatis_plan_t p, const float* x, con
                                            int32_t n_rows, float* y, uint32_t* peaks, float limit,
                                            float* r_out, uint8_t* states_out, tomatis_plan_t prev_plan,
                                            float* prev_y, const uint32_t* prev_peaks, void* hs) {
-  if (!p || !x || !gains || !y || !peaks || !r_out || !states_out || n_rows != 2 ||
+  if (!p || !x || !gains || !y || !peaks || !r_out || !states_out ||
       !(limit > 0.f) || (prev_y && (!prev_peaks || prev_y == y || prev_peaks == peaks)))
     return TOMATIS_E_ARG;
-  // the kernel's partner-rescale instantiation: interior loop, two LDS gain rows,
-  // hop <= 512 (gated_eligible), per-chunk accounting
+  // the kernel's partner-rescale instantiations (gated_eligible): n_fft 2048
+  // interior loop, two LDS gain rows, hop <= 512; n_fft 4096, hop 1024;
+  // per-chunk accounting
   if (!gated_eligible(p) || p->total_chunks <= 0 || !p->chunk_need || p->SH > 8)
     return TOMATIS_E_UNSUPPORTED;
+  if (!gated_rows_ok(p, n_rows)) return TOMATIS_E_ARG;
   const tomatis_plan_s* q = prev_plan ? prev_plan : p;
   if (prev_y && !prev_plan_ok(p, q)) return TOMATIS_E_UNSUPPORTED;
   const GateOut g{r_out, states_out, true};

@@ -96,6 +96,14 @@ struct MainArgs {
   const int32_t* gcarry;  // per run: state id before its first frame (< 0: unresolved,
                           // kGateChained: compose gtf from the nearest resolved run)
   const uint16_t* gtf;    // chained runs' transfer tables [run][gate_D + 2]
+  // cross-fade gate (alpha mode 1, n_fft 4096): gate_xf >= 0 cross-fade frames
+  // (-1: standard gate, gain row = state); every frame's alpha (float64,
+  // process_tomatis_xfade.py:251-274) to a_out, the gain row from alpha; each
+  // run starts from k_gate_carry's alpha before its first frame (gacarry)
+  int gate_xf;
+  double gate_astep;    // 1.0 / gate_xf (gate_xf > 0), computed once on the host
+  double* a_out;
+  const double* gacarry;
 };
 // (also zeroes A.peaks[0, n_zero): this pipelined launch's chunk peaks)
 void launch_r2_plan(const MainArgs& A, uint32_t* pieces, int n_zero, int P, hipStream_t s);
@@ -107,8 +115,10 @@ void launch_prev_runs(const MainArgs& A, int N, hipStream_t s);
 // previous run's start when gtf is given) before a run is left unresolved.
 // gtf (optional): per-run transfer tables [n_runs][gate_D + 2] for chained
 // runs, composed in the transform's prologue (gate_chain_carry)
+// n_fft 2048 (P 64, NR 32) and 4096 (P 128, NR 32; A.gate_xf >= 0: also the
+// alpha before each run's first frame into gacarry, no chaining)
 void launch_gate_carry(const MainArgs& A, int P, int SH, int ch, int32_t* gcarry,
-                       uint16_t* gtf, hipStream_t s);
+                       uint16_t* gtf, double* gacarry, hipStream_t s);
 constexpr int kGateLookback = 512;       // look-back limit of a run that cannot chain
 constexpr int kGateLookbackMax = 4096;   // chained runs: frames back to the previous run's start
 constexpr int kGateChainStates = 1024;   // chaining needs gate_D + 2 <= this (transfer tables)

@@ -378,6 +378,99 @@ __device__ __forceinline__ float lv_frame_r(float lw) {
   return lv_sqrt_fast(lv_opq(mean) + kEps32);  // mean + EPS >= 1e-12 (or NaN / inf)
 }
 
+// ---- n_fft 4096: a 32-leaf window ----
+// lanes 0..31 hold the frame's leaves in order; FWD: drop the oldest LB, append
+// the new block's (lanes 32 - LB + l <- lane 8 l of nl); !FWD (backward
+// scan): prepend at lanes 0..LB-1, drop the newest.  The shift crosses the
+// 16-lane DPP rows: ds_bpermute.
+template <int LB, bool FWD>
+__device__ __forceinline__ float lv_window32(float lw, float nl, int lane) {
+  const int src = FWD ? min(lane + LB, 63) : max(lane - LB, 0);
+  float w = __int_as_float(__builtin_amdgcn_ds_bpermute(src * 4, __float_as_int(lw)));
+#pragma unroll
+  for (int l = 0; l < LB; ++l) {
+    const int v = __builtin_amdgcn_readlane(__float_as_int(nl), 8 * l);
+    __asm__("v_writelane_b32 %0, %1, %2" : "+v"(w) : "s"(v), "n"(FWD ? 32 - LB + l : l));
+  }
+  return w;
+}
+// frame r from a 32-leaf window: numpy's pairwise tree (two 16-leaf trees as
+// lv_frame_r's, then their sum), mean over 4096, + EPS, sqrt; wave-uniform
+__device__ __forceinline__ float lv_frame_r32(float lw) {
+  float t = lw + dpp<kDppRowShl<1>>(lw);
+  t = t + dpp<kDppRowShl<2>>(t);
+  t = t + dpp<kDppRowShl<4>>(t);
+  t = t + dpp<kDppRowShl<8>>(t);
+  const float t0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t), 0));
+  const float t1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t), 16));
+  const float mean = (t0 + t1) * (1.0f / 4096.0f);  // exact (n = 2^12)
+  return lv_sqrt_fast(lv_opq(mean) + kEps32);
+}
+// window / frame r of a W-leaf window (W = n_fft / 128: 16 or 32); LB leaves per block
+template <int W, int LB, bool FWD>
+__device__ __forceinline__ float lv_win(float lw, float nl, int lane) {
+  if constexpr (W == 16) return lv_window<2 * LB, FWD>(lw, nl);
+  else return lv_window32<LB, FWD>(lw, nl, lane);
+}
+template <int W>
+__device__ __forceinline__ float lv_r(float lw) {
+  if constexpr (W == 16) return lv_frame_r(lw);
+  else return lv_frame_r32(lw);
+}
+
+// ---- n_fft 4096 in the transform (P = 128: two waves per frame; lane
+// l = L & 63 of wave w holds sample 64 w + l of every 128-sample leaf) ----
+// per sequence: [leaf q][chain c][position i] (16 positions, chains padded)
+constexpr int kL2CS = 20, kL2LS = 8 * kL2CS;
+// m^2 of the hop block in the last SH registers of v (leaf q = register
+// NRV - SH + q) to scr: chain (64 w + l) & 7, position (64 w + l) >> 3.  The
+// same per-sample arithmetic as lv_leaves (the short sqrt unless the wave holds
+// a 0 < a < 2^-96); the partner wave writes the other 8 positions of each chain
+template <int CH, int SH, int NRV>
+__device__ __forceinline__ void lv_put128(const cf (&v)[NRV], float* scr, int l, int w) {
+  float a[SH];
+  uint32_t umin = 0xffffffffu;
+#pragma unroll
+  for (int j = 0; j < SH; ++j) {
+    a[j] = lv_a<CH>(v[NRV - SH + j]);
+    umin = min(umin, __float_as_uint(a[j]) - 1u);
+  }
+  const int e = 64 * w + l;
+  float* const p = scr + (e & 7) * kL2CS + (e >> 3);
+  if (__builtin_amdgcn_ballot_w64(umin < kLvTiny) == 0) {
+#pragma unroll
+    for (int j = 0; j < SH; ++j) {
+      const float m = lv_sqrt_fast(a[j]);
+      p[j * kL2LS] = m * m;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < SH; ++j) {
+      const float m = lv_sqrt_any(a[j]);
+      p[j * kL2LS] = m * m;
+    }
+  }
+}
+// leaf sums of the SH leaves in scr (both waves' lv_put128 ordered before this
+// by a pair barrier): lane 8 q holds leaf q -- each lane sums one chain's 16
+// positions in order, then the 8 chains as numpy combines its accumulators
+// ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) (lv_leaves' tree)
+template <int SH>
+__device__ __forceinline__ float lv_chains128(const float* scr, int l) {
+  const int q = min(l >> 3, SH - 1);
+  const float4* p = reinterpret_cast<const float4*>(scr + q * kL2LS + (l & 7) * kL2CS);
+  const float4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+  float a0 = q0.x;
+  a0 = a0 + q0.y; a0 = a0 + q0.z; a0 = a0 + q0.w;
+  a0 = a0 + q1.x; a0 = a0 + q1.y; a0 = a0 + q1.z; a0 = a0 + q1.w;
+  a0 = a0 + q2.x; a0 = a0 + q2.y; a0 = a0 + q2.z; a0 = a0 + q2.w;
+  a0 = a0 + q3.x; a0 = a0 + q3.y; a0 = a0 + q3.z; a0 = a0 + q3.w;
+  a0 = a0 + dpp<kDppXor1>(a0);
+  a0 = a0 + dpp<kDppXor2>(a0);
+  a0 = a0 + dpp<kDppHalfMirror>(a0);
+  return a0;
+}
+
 // read-only (for the kernel's lifetime) data through the scalar cache: a
 // constant-address-space view makes uniform loads s_load (lgkmcnt-counted)
 typedef __attribute__((address_space(4))) const uint32_t cu32;
@@ -443,6 +536,8 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   // PR: one hop block per sequence for the partner rescale (LDS-DMA target;
   // n_fft 4096 has no LDS left and takes the blocks through VGPRs)
   __shared__ __attribute__((aligned(16))) char s_pbuf[PR && P == 64 ? NSEQ * SH * P * CH * 4 : 16];
+  // GT at n_fft 4096: per sequence the m^2 of a hop block's leaves (lv_put128)
+  __shared__ __attribute__((aligned(16))) float s_lv[GT && P == 128 ? NSEQ * SH * kL2LS : 4];
   for (int i = threadIdx.x; i < NR * P; i += WG) s_twN[i] = A.twN[i];
   if constexpr (LT) {  // [m/2][l][m&1] = W_P^{(l%8)*m}
     for (int i = threadIdx.x; i < 8 * P; i += WG) {
@@ -508,17 +603,26 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   const float iscale = S.in_scale;
 
   // ---- in-kernel gate: carry-in state from k_gate_carry ----
-  static_assert(!GT || (P == 64 && NR == 32 && (SH == 4 || SH == 8)),
-                "in-kernel levels: n_fft 2048, hop 256 / 512");
+  static_assert(!GT || (P == 64 && NR == 32 && (SH == 4 || SH == 8)) ||
+                    (P == 128 && NR == 32 && SH == 8),
+                "in-kernel levels: n_fft 2048 with hop 256 / 512, n_fft 4096 with hop 1024");
   constexpr int NBLK = NR / SH;  // hop blocks per frame
-  float lw = 0.f;                // lanes 0..15: the current frame's leaf sums
+  // n_fft 4096 (two waves per frame): the leaves of a hop block go through
+  // s_lv, the cross-fade alpha (A.gate_xf >= 0) is stepped in-kernel
+  constexpr bool GX = GT && P == 128;
+  static_assert(!GX || FX2, "n_fft 4096 in-kernel levels: the single-trade FFT's pair counter");
+  float lw = 0.f;                // lanes 0..15 (0..31 at 4096): the current frame's leaf sums
   int gid = 0;                   // gate state id (tm_gate.h)
+  double alpha = 0.0;            // GX: cross-fade alpha after the previous frame
   if constexpr (GT) {
     gid = __builtin_amdgcn_readfirstlane(A.gcarry[run_id]);
     if (gid == kGateChained) gid = gate_chain_carry(A, run_id);
     if (gid < 0) {  // look-back did not resolve: the host re-runs the two-pass path
       if (L == 0) atomicOr(A.err, TOMATIS_ERR_GATE_CARRY);
       gid = 0;
+    }
+    if constexpr (GX) {
+      if (A.gate_xf >= 0) alpha = A.gacarry[run_id];
     }
   }
   float* const lscr = reinterpret_cast<float*>(buf);  // leaf scratch (free at the frame top)
@@ -539,11 +643,9 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   // when present, so the frame loop does not hold 10 more SGPRs
   const uint32_t g_on = S.on_bits, g_off = S.off_bits;
   const bool g_exc = (S.n_on_exc | S.n_off_exc) != 0;
-  // frame k: leaves of its newest block (the last SH registers of fr), r,
-  // predicate, state; r and state of emitted frames stored by lane 0
-  auto gate_frame = [&](const cf (&fr)[NR], int64_t k, bool emit) -> uint32_t {
-    lw = lv_window<SH, true>(lw, lv_leaves<CH, SH, NR>(fr, lscr, L));
-    const float r = lv_frame_r(lw);
+  // frame k from its r: predicate, state (and alpha); r, state (alpha) of
+  // emitted frames stored by lane 0; the gain row
+  auto gate_r = [&](float r, int64_t k, bool emit) -> uint32_t {
     // r is wave-uniform: its bits through readfirstlane keep the predicate and
     // the automaton in SGPRs / SALU
     const uint32_t b = __builtin_amdgcn_readfirstlane(__float_as_uint(r));
@@ -555,12 +657,54 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
     }
     gid = gate_step(gid, pr, A.gate_D);
     const bool c2 = gid == A.gate_D + 1;
+    uint32_t row = c2 ? 1u : 0u;
+    if constexpr (GX) {
+      // process_tomatis_xfade.py:262-278: alpha toward the state's target, the
+      // gain row from alpha (pure rows 0 / 1, lattice rows 2 + m)
+      const int xf = A.gate_xf;
+      if (xf >= 0) {
+        const double tgt = c2 ? 1.0 : 0.0;
+        alpha = xf > 0 ? alpha_step(alpha, tgt, A.gate_astep) : tgt;
+        row = xfade_row(alpha, xf);
+      }
+    }
     if (emit && L == 0) {
       const int64_t fo = S.frame_base + k;
       A.r_out[fo] = r;
       A.st_out[fo] = (uint8_t)(c2 ? 2 : 1);
+      if constexpr (GX) {
+        if (A.gate_xf >= 0) A.a_out[fo] = alpha;
+      }
     }
-    return c2 ? 1u : 0u;
+    return row;
+  };
+  // frame k: leaves of its newest block (the last SH registers of fr), r, gate
+  auto gate_frame = [&](const cf (&fr)[NR], int64_t k, bool emit) -> uint32_t {
+    lw = lv_window<SH, true>(lw, lv_leaves<CH, SH, NR>(fr, lscr, L));
+    return gate_r(lv_frame_r(lw), k, emit);
+  };
+  // n_fft 4096: lv_put128 of the frame's newest block went to s_lv and a pair
+  // barrier ordered both waves' writes before this (both waves read every leaf
+  // and step the same gate); the partner overwrites s_lv only after this
+  // frame's FFT trades, i.e. after these reads
+  const int Lw = L & 63, Wv = __builtin_amdgcn_readfirstlane(L >> 6);
+  float* const lv2 = s_lv + (GX ? seq * SH * kL2LS : 0);
+  auto gate_frame128 = [&](int64_t k, bool emit) -> uint32_t {
+    lw = lv_window32<SH, true>(lw, lv_chains128<SH>(lv2, Lw), Lw);
+    return gate_r(lv_frame_r32(lw), k, emit);
+  };
+  // n_fft 4096, the run's first frame: the leaves of its first NBLK - 1 blocks
+  // (two pair barriers per block: written by both waves, read by both)
+  uint32_t* const pctr = reinterpret_cast<uint32_t*>(reinterpret_cast<float*>(buf) + 2 * kXBuf);
+  auto start_window128 = [&](const cf (&fr)[NR]) {
+    lw = 0.f;
+    sfor<0, NBLK - 1>([&](auto bb) {
+      constexpr int B = decltype(bb)::value;
+      lv_put128<CH, SH, SH * (B + 1)>(*reinterpret_cast<const cf(*)[SH * (B + 1)]>(&fr[0]), lv2, Lw, Wv);
+      pair_barrier(pctr, A.err);
+      lw = lv_window32<SH, true>(lw, lv_chains128<SH>(lv2, Lw), Lw);
+      pair_barrier(pctr, A.err);
+    });
   };
 
   if (valid && R.ka == 0 && S.first_start > S.out_begin) {  // adaptive: zeros before frame 0
@@ -589,7 +733,8 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
   unsigned long long tlast = __builtin_amdgcn_s_memtime();
 #endif
   // window -> FFT -> gain row -> IFFT -> window, OLA into the accumulator
-  auto transform = [&](cf (&v)[NR], uint32_t row) {
+  // row_of(): the frame's gain row, asked for after the forward FFT
+  auto transform = [&](cf (&v)[NR], auto row_of) {
       // ---- analysis window (x * in_scale first, two roundings as the reference) ----
       if (iscale != 1.0f) {
   #pragma unroll
@@ -610,6 +755,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       else fft_fwd<P, NR, LT>(v, L, s_twN, s_twP, buf, A.err);
       TPROF(2, v[NR - 1].x);
       // ---- gain row (real, even, 1/N folded in), per-lane layout ----
+      const uint32_t row = row_of();
       bool g_lds = GM == 1;
       if constexpr (GM == 2) g_lds = row == A.lds_row[0] || row == A.lds_row[1];
       if (g_lds) {
@@ -703,6 +849,8 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
     }
   }
   constexpr bool PL = PR && P == 64;  // the partner's blocks by LDS-DMA (fast loop)
+  // list entry of frame it (entry np past the list: empty resource)
+  auto pent = [&](int it) { return min(it, np); };
   if (fast_run) {
     // Interior run (host-marked): every frame of [kfirst, kb) reads a full frame
     // and every emitted hop block is a full interior block (no stream edges, no
@@ -799,7 +947,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       if constexpr (PL) {
         // piece it of the partner -> LDS slot (branch-free: past the list the
         // resource is empty, the load returns zeros and the store drops)
-        const int blk = (int)plist[2 + 2 * min(it, np)];
+        const int blk = (int)plist[2 + 2 * pent(it)];
         const __amdgpu_buffer_rsrc_t rpl =
             mk_rsrc(yP + (int64_t)blk * (HOP * CH), it < np ? (uint32_t)HOPB : 0u);
 #pragma unroll
@@ -809,7 +957,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
               u * 1024, 0, 2);
       }
       TPROF(0, v[0].x);
-      transform(v, row);
+      transform(v, [&] { return row; });
       TPROF(5, v[NR - 1].x);
       // a frame that starts a new chunk flushes the previous chunk's peak first
       // (pk holds frames < k only)
@@ -847,8 +995,8 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
         constexpr int kAfter = NO + 2 * SH;
         static_assert(kAfter < 63, "vmcnt range");
         __asm__ volatile("s_waitcnt vmcnt(%0)" ::"n"(kAfter) : "memory");
-        const int blk = (int)plist[2 + 2 * min(it, np)];
-        const float sc = __uint_as_float(plist[3 + 2 * min(it, np)]);
+        const int blk = (int)plist[2 + 2 * pent(it)];
+        const float sc = __uint_as_float(plist[3 + 2 * pent(it)]);
         const __amdgpu_buffer_rsrc_t rps =
             mk_rsrc(yP + (int64_t)blk * (HOP * CH), it < np ? (uint32_t)HOPB : 0u);
 #pragma unroll
@@ -918,6 +1066,16 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
     constexpr int PQ = PV ? HOPB / (16 * P) : 1;  // b128 per lane per block
     static_assert(!PV || HOPB % (16 * P) == 0, "a hop block is whole b128 per lane");
 
+    if constexpr (GX) {
+      // the run's first frame's leaves, before the loop (its pair barriers --
+      // volatile asm with a memory clobber -- inside the loop body constrain
+      // the scheduling of every iteration)
+      if (nit > 0) {
+        cf v0[NR];
+        load_frame(kfirst, v0);
+        start_window128(v0);
+      }
+    }
     for (int it = 0; it < nit; ++it) {
       const int64_t k = kfirst + it;
       const bool live = valid && (k < R.kb);
@@ -941,18 +1099,29 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       __amdgpu_buffer_rsrc_t rpp;
       float psc = 1.f;
       if constexpr (PV) {
-        const int blk = (int)plist[2 + 2 * min(it, np)];
-        psc = __uint_as_float(plist[3 + 2 * min(it, np)]);
+        const int blk = (int)plist[2 + 2 * pent(it)];
+        psc = __uint_as_float(plist[3 + 2 * pent(it)]);
         rpp = mk_rsrc(yP + (int64_t)blk * (HOP * CH), it < np ? (uint32_t)HOPB : 0u);
   #pragma unroll
         for (int u = 0; u < PQ; ++u)
           pbk[u] = __builtin_amdgcn_raw_buffer_load_b128(rpp, L * 16, u * 16 * P, 2);  // (nt)
       }
-      if constexpr (GT) {
-        if (it == 0) lw = start_window(v);
-        row = gate_frame(v, k, live && k >= R.ka);
+      if constexpr (GX) {
+        // n_fft 4096: the new block's m^2 into s_lv, a pair barrier, then its
+        // leaves, r, gate and alpha: the gain row is known before the forward
+        // FFT, so its L2 loads issue early (asked for after the FFT, the row
+        // exposed their latency every frame)
+        lv_put128<CH, SH, NR>(v, lv2, Lw, Wv);
+        pair_barrier(pctr, A.err);
+        row = gate_frame128(k, live && k >= R.ka);
+        transform(v, [&] { return row; });
+      } else {
+        if constexpr (GT) {
+          if (it == 0) lw = start_window(v);
+          row = gate_frame(v, k, live && k >= R.ka);
+        }
+        transform(v, [&] { return row; });
       }
-      transform(v, row);
       if constexpr (PV) {
   #pragma unroll
         for (int u = 0; u < PQ; ++u) {
@@ -1139,7 +1308,7 @@ __global__ __launch_bounds__(64) void k_prev_runs(MainArgs A, int N) {
 
 // In-kernel gate, part 1 (tomatis_stft_ola_gated): per run, the gate state
 // before its first frame kf = max(0, ka - rmax + 1), from which the fused
-// kernel continues frame by frame (its 16-leaf window it builds from its own
+// kernel continues frame by frame (its leaf window it builds from its own
 // first frame's registers).  The gate
 // automaton forgets its past at an anchor frame: a frame that is not "on" and
 // "off" leaves C1 idle whatever came before, and D + 1 consecutive frames "on"
@@ -1150,7 +1319,8 @@ __global__ __launch_bounds__(64) void k_prev_runs(MainArgs A, int N) {
 // C1 idle, src/process_tomatis.py:288-289) or kGateLookback frames (then the
 // run is left unresolved, carry = -1, and the host falls back to the two-pass
 // path); the state then runs forward over the recorded predicates to kf.
-// Blocks are prefetched 4 ahead.
+// Blocks are prefetched 4 ahead.  n_fft = 64 NR (2048: NR 32, a 16-leaf
+// window; 4096: NR 64, 32 leaves), hop = 64 SH.
 // Chained runs: a look-back that reaches kc, the first frame of the previous
 // run of the same stream, without an anchor needs no more frames -- the state
 // before kf is the state before kc (that run's own carry-in) stepped over the
@@ -1160,10 +1330,25 @@ __global__ __launch_bounds__(64) void k_prev_runs(MainArgs A, int N) {
 // transform's prologue composes them (gate_chain_carry).  Only a run whose
 // look-back exceeds kGateLookbackMax frames (or nst > kGateChainStates) stays
 // unresolved (carry -1: the host's two-pass fallback).
-template <int CH, int SH>
+// Cross-fade (A.gate_xf >= 0, process_tomatis_xfade.py:251-274): the run also
+// needs alpha before kf.  J = xf + 2 consecutive frames of one state pin alpha
+// to that state's target whatever it was (k_alpha_sync), and frames before 0
+// count as C1 with alpha 0.  So at an anchor the walk replays the states
+// forward and looks for such a run of equal states among the frames whose
+// state it knows; alpha then steps (float64, the reference's operations) from
+// there to kf - 1 (acarry).  Without one the walk goes on to an earlier
+// anchor (the replay is tried at anchors whose distance has doubled since the
+// last try), up to kXfLookback frames; no chaining.
+constexpr int kXfLookback = 1024;
+template <int CH, int SH, int NR>
 __global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restrict__ carry,
-                                                   uint16_t* __restrict__ tf) {
-  constexpr int P = 64, NR = 32, HOP = SH * P, NB = NR / SH, LB = SH / 2, PFD = 4;
+                                                   uint16_t* __restrict__ tf,
+                                                   double* __restrict__ acarry) {
+#ifndef TM_GC_PFD
+#define TM_GC_PFD 4
+#endif
+  constexpr int P = 64, HOP = SH * P, NB = NR / SH, LB = SH / 2, PFD = TM_GC_PFD, W = NR / 2;
+  constexpr float kInvN = 1.0f / (64 * NR);
   __shared__ __attribute__((aligned(16))) float scr[LB * kLvLS];
   __shared__ uint8_t prs[kGateLookbackMax];
   const int run = blockIdx.x;
@@ -1172,14 +1357,18 @@ __global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restri
   const Run R = A.runs[run];
   const TomatisStream S = A.st[R.s];
   const int D = A.gate_D;
+  const int xf = A.gate_xf;  // >= 0: cross-fade alpha
+  const bool xa = xf >= 0;
+  const int J = xf + 2;
+  const double astep = A.gate_astep;
   const int64_t kf = max<int64_t>(0, R.ka - (A.rmax - 1));
   // chain point: the first frame of the previous run of this stream (runs are
   // in stream / frame order); 0 for a stream's first run (the stream start
   // anchors it).  Without a tf table the walk keeps the kGateLookback limit.
   int64_t kc = 0;
   if (run > 0 && A.runs[run - 1].s == R.s) kc = max<int64_t>(0, A.runs[run - 1].ka - (A.rmax - 1));
-  const bool can_chain = tf != nullptr && kc > 0 && kf - kc <= kGateLookbackMax;
-  const int cap = can_chain ? kGateLookbackMax : kGateLookback;
+  const bool can_chain = !xa && tf != nullptr && kc > 0 && kf - kc <= kGateLookbackMax;
+  const int cap = xa ? kXfLookback : (can_chain ? kGateLookbackMax : kGateLookback);
   const __amdgpu_buffer_rsrc_t rx =
       mk_rsrc(A.x + S.in_off, (uint32_t)min<int64_t>(S.n * CH * 4, 0x7fffffffll));
   auto load_block = [&](int64_t b, cf (&dst)[SH]) {  // block b of the frame grid
@@ -1204,6 +1393,36 @@ __global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restri
     const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e), 48));
     return (r0 + r1) + (r2 + r3);
   };
+  // cross-fade: from anchor ak (the state after frame ak is aid; ak = -1:
+  // before frame 0, alpha 0 there) over the recorded predicates of frames
+  // (ak, kf): the state id and alpha before kf; false when no run of J equal
+  // known states pins alpha
+  double a_res = 0.0;
+  int id_res = 0;
+  auto replay_xf = [&](int64_t ak, int aid) -> bool {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    int id = aid, st = (aid == D + 1) ? 2 : 1, rl = 1;
+    bool pin = ak < 0 || xf == 0;
+    double a = ak < 0 ? 0.0 : (st == 2 ? 1.0 : 0.0);
+    for (int64_t k = ak + 1; k < kf; ++k) {
+      id = gate_step(id, prs[kf - 1 - k], D);
+      const int s2 = (id == D + 1) ? 2 : 1;
+      rl = (s2 == st) ? rl + 1 : 1;
+      st = s2;
+      const double tgt = st == 2 ? 1.0 : 0.0;
+      if (pin) {
+        a = xf > 0 ? alpha_step(a, tgt, astep) : tgt;
+      } else if (rl >= J) {
+        pin = true;
+        a = tgt;
+      }
+    }
+    id_res = id;
+    a_res = a;
+    return pin;
+  };
   // frame kf - 1 = blocks kf - 1 .. kf + NB - 2: their energies for the fast
   // walk (the exact leaf window only if the exact walk runs: the transform
   // builds its own from its first frame's registers)
@@ -1217,10 +1436,28 @@ __global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restri
     for (int i = 0; i < NB; ++i) eb[i] = block_energy(b[i]);
   }
   int id = 0;
+  double alpha = 0.0;
   if (kf > 0) {
     int64_t j = kf - 1;          // the window holds frame j
     int64_t a_k = -2;            // anchor: the state after frame a_k is a_id (-2: none)
     int a_id = 0, on_run = 0, n = 0;
+    int next_try = 0;            // cross-fade: replay at an anchor once n >= next_try
+    // an anchor at frame ak (state aid after it) ends the walk: always for the
+    // standard gate; for the cross-fade only if the replay pins alpha
+    auto take = [&](int64_t ak, int aid) -> bool {
+      if (!xa) {
+        a_k = ak;
+        a_id = aid;
+        return true;
+      }
+      if (ak >= 0 && n < next_try) return false;
+      if (replay_xf(ak, aid)) {
+        a_k = -4;  // resolved with alpha (id_res, a_res)
+        return true;
+      }
+      next_try = 2 * n;
+      return false;
+    };
     cf bq[PFD][SH];              // blocks j - 1 - u, prefetched
     sfor<0, PFD>([&](auto uu) { load_block(j - 1 - decltype(uu)::value, bq[decltype(uu)::value]); });
     // Fast walk: the predicate of each frame from an approximate r (block
@@ -1240,7 +1477,7 @@ __global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restri
             float es = 0.f;
 #pragma unroll
             for (int i = 0; i < NB; ++i) es += eb[i];
-            const float ra = sqrtf(es * (1.0f / 2048.0f) + kEps32);
+            const float ra = sqrtf(es * kInvN + kEps32);
             const bool on_s = ra >= t_on * (1.f + kM), non_s = ra < t_on * (1.f - kM);
             const bool off_s = ra <= t_off * (1.f - kM), noff_s = ra > t_off * (1.f + kM);
             if (!(on_s || non_s) || !(off_s || noff_s)) {
@@ -1251,18 +1488,12 @@ __global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restri
               if (L == 0) prs[n] = pr;
               ++n;
               on_run = (on_s && !off_s) ? on_run + 1 : 0;
-              if (!on_s && off_s) {
-                a_k = j;
-                a_id = 0;
+              if (!on_s && off_s && take(j, 0)) {
                 go = false;
-              } else if (on_run == D + 1) {
-                a_k = j + D;
-                a_id = D + 1;
+              } else if (on_run == D + 1 && take(j + D, D + 1)) {
                 go = false;
               } else if (j == 0) {
-                a_k = -1;
-                a_id = 0;
-                go = false;
+                go = !take(-1, 0);  // (always resolves)
               } else if (can_chain && j == kc) {
                 a_k = -3;  // chained: frames [kc, kf) recorded
                 go = false;
@@ -1287,12 +1518,13 @@ __global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restri
       a_id = 0;
       on_run = 0;
       n = 0;
+      next_try = 0;
       {
         cf b[NB][SH];
 #pragma unroll
         for (int i = 0; i < NB; ++i) load_block(kf - 1 + i, b[i]);
 #pragma unroll
-        for (int i = 0; i < NB; ++i) lw = lv_window<SH, true>(lw, lv_leaves<CH, SH, SH>(b[i], scr, L));
+        for (int i = 0; i < NB; ++i) lw = lv_win<W, LB, true>(lw, lv_leaves<CH, SH, SH>(b[i], scr, L), L);
       }
       sfor<0, PFD>([&](auto uu) { load_block(j - 1 - decltype(uu)::value, bq[decltype(uu)::value]); });
     }
@@ -1301,29 +1533,23 @@ __global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restri
       sfor<0, PFD>([&](auto uu) {
         constexpr int u = decltype(uu)::value;
         if (more) {
-          const uint8_t pr = gate_pred(lv_frame_r(lw), S);
+          const uint8_t pr = gate_pred(lv_r<W>(lw), S);
           if (L == 0) prs[n] = pr;
           ++n;
           on_run = ((pr & 1) && !(pr & 2)) ? on_run + 1 : 0;
-          if (!(pr & 1) && (pr & 2)) {
-            a_k = j;  // sync: C1 idle after j
-            a_id = 0;
-            more = false;
-          } else if (on_run == D + 1) {
-            a_k = j + D;  // D + 1 frames on: C2 after j + D
-            a_id = D + 1;
-            more = false;
+          if (!(pr & 1) && (pr & 2) && take(j, 0)) {
+            more = false;  // sync: C1 idle after j
+          } else if (on_run == D + 1 && take(j + D, D + 1)) {
+            more = false;  // D + 1 frames on: C2 after j + D
           } else if (j == 0) {
-            a_k = -1;  // stream start: C1 idle before frame 0
-            a_id = 0;
-            more = false;
+            more = !take(-1, 0);  // stream start: C1 idle before frame 0
           } else if (can_chain && j == kc) {
             a_k = -3;  // chained: frames [kc, kf) recorded
             more = false;
           } else if (n >= cap) {
             more = false;  // unresolved
           } else {
-            lw = lv_window<SH, false>(lw, lv_leaves<CH, SH, SH>(bq[u], scr, L));
+            lw = lv_win<W, LB, false>(lw, lv_leaves<CH, SH, SH>(bq[u], scr, L), L);
             load_block(j - 1 - PFD, bq[u]);
             --j;
           }
@@ -1333,7 +1559,10 @@ __global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restri
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (a_k == -2) {
+    if (a_k == -4) {
+      id = id_res;
+      alpha = a_res;
+    } else if (a_k == -2) {
       id = -1;
     } else if (a_k == -3) {
       // transfer function over frames [kc, kf): lane s replays from state s
@@ -1349,7 +1578,10 @@ __global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restri
       for (int64_t k = a_k + 1; k < kf; ++k) id = gate_step(id, prs[kf - 1 - k], D);
     }
   }
-  if (L == 0) carry[run] = id;
+  if (L == 0) {
+    carry[run] = id;
+    if (xa) acarry[run] = alpha;
+  }
 }
 
 // Generic hop: same transform, windowed frame outputs to scratch, then a gather.
@@ -1715,6 +1947,19 @@ void launch_main_pf(const MainArgs& A, int ch, hipStream_t s) {
       return;
     }
   }
+  if constexpr (P == 128 && NR == 32 && WG == 512 && SH == 8) {
+    if (A.gated) {  // in-kernel levels + gate (+ cross-fade alpha), n_fft 4096, hop 1024
+      if (A.yprev) {
+        if (ch == 2) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 0, PF, NT, WG, true, true>), g, b, 0, s, A);
+        else hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, 0, PF, NT, WG, true, true>), g, b, 0, s, A);
+      } else if (ch == 2) {
+        hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 0, PF, NT, WG, false, true>), g, b, 0, s, A);
+      } else {
+        hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 1, 0, PF, NT, WG, false, true>), g, b, 0, s, A);
+      }
+      return;
+    }
+  }
   if constexpr (P == 128 && NR == 32 && WG == 512 && SH <= 8) {
     if (A.yprev) {  // pipelined batch, n_fft 4096 (gain rows in L2; partner blocks in VGPRs)
       if (ch == 2) hipLaunchKernelGGL((k_stft_ola<P, NR, SH, 2, 0, PF, NT, WG, true>), g, b, 0, s, A);
@@ -1887,15 +2132,19 @@ void launch_prev_runs(const MainArgs& A, int N, hipStream_t s) {
 }
 
 void launch_gate_carry(const MainArgs& A, int P, int SH, int ch, int32_t* gcarry,
-                       uint16_t* gtf, hipStream_t s) {
-  if (A.n_runs <= 0 || P != 64) return;
+                       uint16_t* gtf, double* gacarry, hipStream_t s) {
+  if (A.n_runs <= 0) return;
   const dim3 g(A.n_runs), b(64);
-  if (SH == 8) {
-    if (ch == 2) hipLaunchKernelGGL((k_gate_carry<2, 8>), g, b, 0, s, A, gcarry, gtf);
-    else hipLaunchKernelGGL((k_gate_carry<1, 8>), g, b, 0, s, A, gcarry, gtf);
-  } else if (SH == 4) {
-    if (ch == 2) hipLaunchKernelGGL((k_gate_carry<2, 4>), g, b, 0, s, A, gcarry, gtf);
-    else hipLaunchKernelGGL((k_gate_carry<1, 4>), g, b, 0, s, A, gcarry, gtf);
+  // (the look-back reads blocks in the P = 64 layout: hop = 64 x its SH)
+  if (P == 64 && SH == 8) {
+    if (ch == 2) hipLaunchKernelGGL((k_gate_carry<2, 8, 32>), g, b, 0, s, A, gcarry, gtf, gacarry);
+    else hipLaunchKernelGGL((k_gate_carry<1, 8, 32>), g, b, 0, s, A, gcarry, gtf, gacarry);
+  } else if (P == 64 && SH == 4) {
+    if (ch == 2) hipLaunchKernelGGL((k_gate_carry<2, 4, 32>), g, b, 0, s, A, gcarry, gtf, gacarry);
+    else hipLaunchKernelGGL((k_gate_carry<1, 4, 32>), g, b, 0, s, A, gcarry, gtf, gacarry);
+  } else if (P == 128 && SH == 8) {  // n_fft 4096, hop 1024
+    if (ch == 2) hipLaunchKernelGGL((k_gate_carry<2, 16, 64>), g, b, 0, s, A, gcarry, gtf, gacarry);
+    else hipLaunchKernelGGL((k_gate_carry<1, 16, 64>), g, b, 0, s, A, gcarry, gtf, gacarry);
   }
 }
 

@@ -391,9 +391,11 @@ class GatePipeline:
         """``geometry``: optional per-stream dicts (first_start, n_frames,
         out_begin, out_len, chunk_first, chunk_len, n_chunks) replacing the
         reference schedule -- a time shard of a longer stream (timeshard.py).
-        ``fused_levels``: standard mode computes levels and gate states inside
-        the transform kernel (tomatis_stft_ola_gated) where the library takes
-        the shape; False, or a shape it declines, runs the two-pass chain.
+        ``fused_levels``: levels and gate states (cross-fade: and alpha) are
+        computed inside the transform kernel (tomatis_stft_ola_gated) where the
+        library takes the shape (standard 2048 / 256 or 512; standard or
+        cross-fade 4096 / 1024); False, or a shape it declines, runs the
+        two-pass chain.
         ``pipelined``: successive run() calls form a batch pipeline
         (tomatis_stft_ola_gated_pipelined; the two-pass chain -- xfade, n_fft
         4096 -- through tomatis_stft_ola_pipelined): each pass leaves its output
@@ -482,7 +484,9 @@ class GatePipeline:
         self.n_rows = len(rows)
         self.out_offs = out_offs
         self.g1_db, self.g2_db = g1_db, g2_db
-        self.fused_levels = bool(fused_levels) and not self.xfade
+        self.fused_levels = bool(fused_levels)
+        if self.xfade:  # the gated calls' per-frame alpha (cross-fade plans)
+            check(lib().tomatis_plan_set_gate_alpha(self.plan.h, ptr(self.alpha)), "set_gate_alpha")
         self.gated_used = False   # the last run() took tomatis_stft_ola_gated
         self.gate_fallbacks = 0   # gated passes re-run on the two-pass chain
         self.pipelined = bool(pipelined)
