@@ -1340,7 +1340,7 @@ __global__ __launch_bounds__(64) void k_prev_runs(MainArgs A, int N) {
 // anchor (the replay is tried at anchors whose distance has doubled since the
 // last try), up to kXfLookback frames; no chaining.
 constexpr int kXfLookback = 1024;
-template <int CH, int SH, int NR>
+template <int CH, int SH, int NR, bool XA>
 __global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restrict__ carry,
                                                    uint16_t* __restrict__ tf,
                                                    double* __restrict__ acarry) {
@@ -1357,8 +1357,8 @@ __global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restri
   const Run R = A.runs[run];
   const TomatisStream S = A.st[R.s];
   const int D = A.gate_D;
-  const int xf = A.gate_xf;  // >= 0: cross-fade alpha
-  const bool xa = xf >= 0;
+  const int xf = A.gate_xf;  // XA: cross-fade alpha (xf >= 0)
+  constexpr bool xa = XA;
   const int J = xf + 2;
   const double astep = A.gate_astep;
   const int64_t kf = max<int64_t>(0, R.ka - (A.rmax - 1));
@@ -1445,7 +1445,7 @@ __global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restri
     // an anchor at frame ak (state aid after it) ends the walk: always for the
     // standard gate; for the cross-fade only if the replay pins alpha
     auto take = [&](int64_t ak, int aid) -> bool {
-      if (!xa) {
+      if constexpr (!xa) {
         a_k = ak;
         a_id = aid;
         return true;
@@ -1580,7 +1580,7 @@ __global__ __launch_bounds__(64) void k_gate_carry(MainArgs A, int32_t* __restri
   }
   if (L == 0) {
     carry[run] = id;
-    if (xa) acarry[run] = alpha;
+    if constexpr (xa) acarry[run] = alpha;
   }
 }
 
@@ -2136,16 +2136,24 @@ void launch_gate_carry(const MainArgs& A, int P, int SH, int ch, int32_t* gcarry
   if (A.n_runs <= 0) return;
   const dim3 g(A.n_runs), b(64);
   // (the look-back reads blocks in the P = 64 layout: hop = 64 x its SH)
+#define TM_GC(C, S, R, X) hipLaunchKernelGGL((k_gate_carry<C, S, R, X>), g, b, 0, s, A, gcarry, gtf, gacarry)
   if (P == 64 && SH == 8) {
-    if (ch == 2) hipLaunchKernelGGL((k_gate_carry<2, 8, 32>), g, b, 0, s, A, gcarry, gtf, gacarry);
-    else hipLaunchKernelGGL((k_gate_carry<1, 8, 32>), g, b, 0, s, A, gcarry, gtf, gacarry);
+    if (ch == 2) TM_GC(2, 8, 32, false);
+    else TM_GC(1, 8, 32, false);
   } else if (P == 64 && SH == 4) {
-    if (ch == 2) hipLaunchKernelGGL((k_gate_carry<2, 4, 32>), g, b, 0, s, A, gcarry, gtf, gacarry);
-    else hipLaunchKernelGGL((k_gate_carry<1, 4, 32>), g, b, 0, s, A, gcarry, gtf, gacarry);
-  } else if (P == 128 && SH == 8) {  // n_fft 4096, hop 1024
-    if (ch == 2) hipLaunchKernelGGL((k_gate_carry<2, 16, 64>), g, b, 0, s, A, gcarry, gtf, gacarry);
-    else hipLaunchKernelGGL((k_gate_carry<1, 16, 64>), g, b, 0, s, A, gcarry, gtf, gacarry);
+    if (ch == 2) TM_GC(2, 4, 32, false);
+    else TM_GC(1, 4, 32, false);
+  } else if (P == 128 && SH == 8) {  // n_fft 4096, hop 1024 (cross-fade: alpha too)
+    if (A.gate_xf >= 0) {
+      if (ch == 2) TM_GC(2, 16, 64, true);
+      else TM_GC(1, 16, 64, true);
+    } else if (ch == 2) {
+      TM_GC(2, 16, 64, false);
+    } else {
+      TM_GC(1, 16, 64, false);
+    }
   }
+#undef TM_GC
 }
 
 void launch_lds_gather(const LdsArgs& A, hipStream_t s) {
