@@ -58,6 +58,9 @@ def main():
             for r in csv.DictReader(open(f)):
                 if bk in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE":
                     bv.append(float(r["Counter_Value"]))
+        if "--base-first" in a:  # only the base run's first N dispatches (e.g. the
+            # pipeline's first, unpipelined passes, not bench.py's one-file passes)
+            bv = bv[:int(a[a.index("--base-first") + 1])]
         if not bv:
             sys.exit(f"no FETCH_SIZE dispatches of {kern} under the base run")
         base_kib = sum(bv) / len(bv)
