@@ -967,9 +967,11 @@ __global__ __launch_bounds__(1024) void k_level_stats(const double* __restrict__
   const int64_t n = all ? F : nv;
   if (n == 0) {
     if (tid == 0) {
+      // no frame at all: find_optimal_threshold's np.median(levels) of an
+      // empty array is NaN (process_tomatis_adaptive.py:124-127)
       tlh[3 * s + 0] = __longlong_as_double(0x7ff8000000000000ll);
       tlh[3 * s + 1] = __longlong_as_double(0x7ff8000000000000ll);
-      tlh[3 * s + 2] = 0.0;
+      tlh[3 * s + 2] = __longlong_as_double(0x7ff8000000000000ll);
     }
     return;
   }

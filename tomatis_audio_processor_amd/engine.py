@@ -758,12 +758,18 @@ class AdaptivePipeline:
             k0, F, s0 = dsp.adaptive_frames(N, n_fft, hop)
             st = TomatisStream()
             st.in_off, st.n, st.first_start, st.n_frames = off, N, s0, F
+            # (a stream with no frame -- shorter than n_fft / 2 -- has no output
+            # in the plan; its result is N zeros, below)
             st.out_begin, st.out_len = 0, (N if F else 0)
             st.n_chunks, st.chunk_first, st.chunk_len = 1, 0, 1
             st.in_scale, st.out_scale = 1.0, 1.0
             streams.append(st)
+        # output slices of N samples for every stream: one with no frame
+        # writes N zeros (process_tomatis_adaptive.py:289-334: y = zeros_like,
+        # no frame adds to it, then / max(norm, 1e-8))
+        self.res_lens = list(ss.lens)
         if out is None:
-            self.y, out_offs = _alloc_out(torch, [s.out_len for s in streams], ss.ch, ss.x.device)
+            self.y, out_offs = _alloc_out(torch, self.res_lens, ss.ch, ss.x.device)
         else:
             self.y, out_offs = out[0], list(out[1])
         for st, o in zip(streams, out_offs):
@@ -793,14 +799,25 @@ class AdaptivePipeline:
         self.gains = torch.from_numpy(np.stack(rows)).to(dev)
         self.n_rows = len(rows)
         self.out_offs = out_offs
+        # output slices no kernel writes (streams without frames): zeroed in
+        # every output buffer this pipeline gets
+        self._idle = [(o, N * ss.ch) for o, N, st in zip(out_offs, self.res_lens, streams)
+                      if st.n_frames == 0 and N > 0]
+        self._clear_idle(self.y)
         self.pipelined = bool(pipelined)
         self.pending = False      # pipelined: self.y awaits its limiter
         self._after = None        # run(prev_pipe=...): another pipeline's pending pass
         if self.pipelined:
             self._ys = [self.y, out2 if out2 is not None else
                         (torch.empty_like(self.y) if second_buffer else None)]
+            self._clear_idle(self._ys[1])
             self._pks = [self.peaks, torch.zeros_like(self.peaks)]
             self._cur = 0
+
+    def _clear_idle(self, buf):
+        if buf is not None:
+            for o, n in self._idle:
+                buf[o:o + n].zero_()
 
     def run(self, marks=None, timer=None, check_device: bool = True, prev_pipe=None):
         """``timer`` (a dict) collects synchronised wall-clock phases (profiling).
@@ -842,6 +859,7 @@ class AdaptivePipeline:
         nxt = (1 - self._cur) if self.pending else self._cur
         if self._ys[nxt] is None:  # second_buffer=False, standalone: allocated on first need
             self._ys[nxt] = _torch().empty_like(self._ys[self._cur])
+            self._clear_idle(self._ys[nxt])
         if a is not None and a.pending:
             pplan, prev_y, prev_pk = a.plan, a.y, a.peaks
         elif self.pending:
@@ -1028,7 +1046,7 @@ class AdaptivePipeline:
     def result(self) -> Result:
         self.flush()
         st = list(self.plan.streams)[:self.ss.n_streams]
-        return Result(y=self.y, out_offs=self.out_offs, out_lens=[s.out_len for s in st],
+        return Result(y=self.y, out_offs=self.out_offs, out_lens=list(self.res_lens),
                       ch=self.ss.ch, frame_base=[s.frame_base for s in st],
                       n_frames=[s.n_frames for s in st],
                       first_start=[s.first_start for s in st], hop=self.hop,
@@ -1095,7 +1113,7 @@ class AdaptiveGroups:
         torch = _torch()
         n_fft, hop = params.get("n_fft", 4096), params.get("hop", 2048)
         G = max(1, min(int(groups), ss.n_streams))
-        out_lens = [N if dsp.adaptive_frames(N, n_fft, hop)[1] else 0 for N in ss.lens]
+        out_lens = list(ss.lens)  # (streams without frames: N zeros, AdaptivePipeline)
         self.y, offs = _alloc_out(torch, out_lens, ss.ch, ss.x.device)
         y2 = torch.empty_like(self.y) if (pipelined and second_buffer) else None
         # contiguous groups balanced by samples
@@ -1141,6 +1159,7 @@ class AdaptiveGroups:
                 y2 = torch.empty_like(self.pipes[0]._ys[0])
                 for q in self.pipes:
                     q._ys[1] = y2
+                    q._clear_idle(y2)
         G = len(self.pipes)
         gens = []
         # transforms in group order; the first also waits for every group's
@@ -1189,7 +1208,7 @@ class AdaptiveGroups:
         y0 = self.pipes[0].y
         for p in self.pipes[1:]:
             if p.y.data_ptr() != y0.data_ptr():
-                for o, n in zip(p.out_offs, [s.out_len for s in list(p.plan.streams)[:p.ss.n_streams]]):
+                for o, n in zip(p.out_offs, p.res_lens):
                     y0[o:o + n * p.ss.ch].copy_(p.y[o:o + n * p.ss.ch])
                 p.y = y0
         self.y = y0
