@@ -79,3 +79,93 @@ def test_random_config_vs_oracle(case):
     if not len(y):
         return
     _check_chunks(res, ref, y, yr, _mask_for(case, ref), mode)
+
+
+def _check_chunks_i(res, i, ref, y, yr, m, mode):
+    """test_gpu_parity._check_chunks for stream i of a batch"""
+    from tomatis_audio_processor_amd import conditioning
+    flags, ranges, peaks = res.scale_flags(i), res.chunk_ranges(i), res.stream_peaks(i)
+    ref_scales = ref["scales"] if mode != "adaptive" else [ref["scale"] or 1.0]
+    assert len(ranges) == len(ref_scales) == len(flags)
+    for c, (a, b) in enumerate(ranges):
+        if b <= a:
+            continue
+        gs = float(np.float32(0.999) / np.float32(peaks[c])) if peaks[c] > 0.999 else 1.0
+        rs = float(ref_scales[c] or 1.0)
+        mm = m[a:b]
+        if abs(gs / rs - 1.0) > conditioning.ETA:
+            assert flags[c], f"stream {i} chunk {c}: scale {gs} vs oracle {rs} but not flagged"
+        if not flags[c]:
+            err = np.abs(y[a:b][mm] - yr[a:b][mm])
+        else:
+            err = np.abs(y[a:b][mm] / gs - yr[a:b][mm] / rs) * min(gs, rs)
+        assert float(err.max(initial=0.0)) <= 1e-4, f"stream {i} chunk {c}: {err.max()}"
+
+
+def _batches(n=16, seed=77031):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        mode = ["standard", "xfade", "adaptive"][rng.integers(3)]
+        n_fft, hop = SHAPES[rng.integers(len(SHAPES))]
+        ch = int(rng.choice([1, 2, 2, 3]))
+        if ch > 2 and (n_fft, hop) in ((2048, 512), (2048, 256), (4096, 1024), (4096, 2048)):
+            n_fft, hop = 3000, 750          # > 2 channels: the any-size path
+        sr = int([44100, 48000, 96000][rng.integers(3)])
+        ns = int(rng.integers(1, 6))
+        lens = [max(16, int(float(rng.choice([0.01, 0.2, 1.5, 4.0, 9.0])) * sr)
+                    + int(rng.integers(0, 1500))) for _ in range(ns)]
+        gains = [float(10.0 ** rng.uniform(-3.0, 0.3)) for _ in range(ns)]
+        if mode == "adaptive":
+            params = dict(n_fft=n_fft, hop=hop, xfade_ms=float(rng.choice([0.0, 500.0])),
+                          min_hold_ms=float(rng.choice([0.0, 250.0])))
+        elif mode == "xfade":
+            params = dict(gate_ui=int(rng.integers(30, 70)), gate_offset=-90, n_fft=n_fft, hop=hop,
+                          xfade_ms=float(rng.choice([0.0, 500.0])))
+        else:
+            params = dict(gate_ui=int(rng.integers(30, 70)), n_fft=n_fft, hop=hop)
+        out.append(dict(name=f"b{i:02d}_{mode}_{n_fft}_{hop}_{ch}ch_{ns}x", mode=mode, sr=sr,
+                        ch=ch, lens=lens, gains=gains, seed=5000 + 10 * i, params=params))
+    return out
+
+
+BATCHES = _batches()
+
+
+@pytest.mark.parametrize("case", BATCHES, ids=[c["name"] for c in BATCHES])
+def test_random_batch_vs_oracle(case):
+    """A batch of 1-5 streams of ragged lengths (one launch, per-stream gate,
+    thresholds and limiter chunks) against the oracle run on each stream alone."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from tomatis_audio_processor_amd import engine as E
+    mode, sr, ch = case["mode"], case["sr"], case["ch"]
+    xs = [(synth_stream(case["seed"] + j, n, ch, sr) * np.float32(g)).astype(np.float32)
+          for j, (n, g) in enumerate(zip(case["lens"], case["gains"]))]
+    ss = E.StreamSet.from_arrays(xs, sr)
+    p = dict(case["params"])
+    if mode == "adaptive":
+        pipe = E.AdaptivePipeline(ss, **p)
+    else:
+        pipe = E.GatePipeline(ss, **p)
+    res = pipe.run()
+    torch.cuda.synchronize()
+    for j, x in enumerate(xs):
+        c1 = dict(mode=mode, sr=sr, ch=ch, N=len(x), params=p)
+        ref = run_oracle(c1, None, x)
+        y = res.output(j)
+        yr = np.asarray(ref["y"], np.float64)
+        assert y.shape == yr.shape, (j, y.shape, yr.shape)
+        if mode in ("standard", "xfade"):
+            np.testing.assert_array_equal(res.stream_r(j).view(np.uint32), ref["r"].view(np.uint32))
+            np.testing.assert_array_equal(res.stream_states(j), ref["states"])
+            if mode == "xfade":
+                np.testing.assert_array_equal(res.stream_alpha(j), ref["alpha"])
+        else:
+            np.testing.assert_array_equal(res.stream_states(j), ref["states"])
+            np.testing.assert_array_equal(res.stream_alpha(j), ref["alpha"])
+            np.testing.assert_array_equal(np.float64(res.extra["thresholds"].cpu().numpy()[j]),
+                                          np.float64(ref["threshold"]))
+        if len(y):
+            _check_chunks_i(res, j, ref, y, yr, _mask_for(c1, ref), mode)
