@@ -169,3 +169,51 @@ def test_random_batch_vs_oracle(case):
                                           np.float64(ref["threshold"]))
         if len(y):
             _check_chunks_i(res, j, ref, y, yr, _mask_for(c1, ref), mode)
+
+
+def _eq_cases(n=12, seed=99177):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        n_fft, hop = SHAPES[rng.integers(len(SHAPES))]
+        sr = int([44100, 48000, 96000][rng.integers(3)])
+        ch = int(rng.choice([1, 2]))
+        N = max(32, int(float(rng.choice([0.05, 1.0, 5.0])) * sr) + int(rng.integers(0, 999)))
+        k = int(rng.integers(3, 30))
+        fr = np.sort(rng.uniform(20.0, sr / 2, k)).astype(np.float32)
+        db = rng.uniform(-12.0, 12.0, k).astype(np.float32)
+        out.append(dict(name=f"eq{i:02d}_{n_fft}_{hop}_{ch}ch_{sr}", sr=sr, ch=ch, N=N,
+                        seed=7000 + i, n_fft=n_fft, hop=hop, pad=bool(rng.integers(2)),
+                        gdb=float(rng.choice([0.0, -3.0, 4.5])), fr=fr, db=db,
+                        gain=float(10.0 ** rng.uniform(-2.0, 0.0))))
+    return out
+
+
+EQS = _eq_cases()
+
+
+@pytest.mark.parametrize("case", EQS, ids=[c["name"] for c in EQS])
+def test_random_static_eq_vs_oracle(case):
+    """layer2_apply_eq's static-EQ STFT (src/layer2_apply_eq.py:66-233; pad /
+    no pad as layer-2b) with a random EQ curve, against the oracle: samples
+    within 1e-4 where sum w^2 >= 1e-3."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from oracle import tomatis_oracle as orc
+    from tomatis_audio_processor_amd import dsp, engine as E
+    sr, ch, n_fft, hop = case["sr"], case["ch"], case["n_fft"], case["hop"]
+    x = (synth_stream(case["seed"], case["N"], ch, sr) * np.float32(case["gain"])).astype(np.float32)
+    ref = orc.apply_eq_stft(x, sr, case["fr"], case["db"], n_fft=n_fft, hop=hop, pad=case["pad"],
+                            global_gain_db=case["gdb"])
+    gain = dsp.build_gain_per_bin(sr, n_fft, case["fr"], case["db"])
+    np.testing.assert_array_equal(gain, ref["gain"])
+    pipe = E.StaticEqPipeline(E.StreamSet.from_arrays([x], sr), gain, n_fft=n_fft, hop=hop,
+                              pad=case["pad"], global_gain_db=case["gdb"])
+    res = pipe.run()
+    torch.cuda.synchronize()
+    y, yr = res.output(0), np.asarray(ref["y"], np.float64)
+    assert y.shape == yr.shape
+    m = ref["wsum"] >= 1e-3
+    err = np.abs(y[m] - yr[m])
+    assert float(err.max(initial=0.0)) <= 1e-4, float(err.max())
