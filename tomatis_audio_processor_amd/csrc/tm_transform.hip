@@ -754,6 +754,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
         fftx128_fwd(v, L, s_twN, s_twP[L], s_twP[2 * (L & 31)], reinterpret_cast<float*>(buf), A.err);
       else fft_fwd<P, NR, LT>(v, L, s_twN, s_twP, buf, A.err);
       TPROF(2, v[NR - 1].x);
+      if constexpr (GT && P == 64) __builtin_amdgcn_s_setprio(0);  // (raised for the gate)
       // ---- gain row (real, even, 1/N folded in), per-lane layout ----
       const uint32_t row = row_of();
       bool g_lds = GM == 1;
@@ -939,6 +940,13 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       const bool emit = it >= nwarm;
       uint32_t row;
       if constexpr (GT) {
+        // the in-kernel gate is a latency chain (leaf sums through LDS, DPP
+        // trees, sqrt, readfirstlane, the SALU automaton): the wave runs it and
+        // its forward FFT at raised priority, so the SIMD's other wave fills
+        // the gaps instead of holding the issue slots (C2 -3 %, C4 -6 %,
+        // quiet C2 -6 %: DESIGN.md §6, profiles/r06/prio/); back to 0 after
+        // the forward FFT (transform)
+        __builtin_amdgcn_s_setprio(2);
         row = gate_frame(v, kfirst + it, emit);
       } else {
         row = row_of(rw_nx, it);
@@ -1118,6 +1126,7 @@ __global__ __launch_bounds__(WG, WG / 256 > 2 ? WG / 256 : 2) void k_stft_ola(Ma
       } else {
         if constexpr (GT) {
           if (it == 0) lw = start_window(v);
+          __builtin_amdgcn_s_setprio(2);  // (as the interior loop: until after the forward FFT)
           row = gate_frame(v, k, live && k >= R.ka);
         }
         transform(v, [&] { return row; });
