@@ -487,6 +487,9 @@ __device__ __forceinline__ void x128_trade(cf (&v)[32], int l, float* out, const
                                            uint32_t* ctr, uint32_t* err) {
   float2* o = reinterpret_cast<float2*>(out) + l;
   const float2* q = reinterpret_cast<const float2*>(in) + l;
+  // the partner wave waits at this pair barrier: the trade runs at raised
+  // priority (c5x kernel -1.4 %, DESIGN.md §6 "Wave priority")
+  __builtin_amdgcn_s_setprio(2);
   sfor<0, 16>([&](auto jj) {
     constexpr int J = decltype(jj)::value;
     o[64 * J] = make_float2(v[16 + J].x, v[16 + J].y);
@@ -497,6 +500,7 @@ __device__ __forceinline__ void x128_trade(cf (&v)[32], int l, float* out, const
     const float2 t = q[64 * J];
     v[16 + J] = {t.x, t.y};
   });
+  __builtin_amdgcn_s_setprio(0);
 }
 
 // forward.  buf: the sequence's 2 kXBuf regions (H_0, H_1) then the counter;
